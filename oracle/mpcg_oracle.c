@@ -1,0 +1,898 @@
+/*
+ * mpcg_oracle.c — CPU restatement (plain C99) of the reference's per-guess
+ * SQP solve.  TEST INFRASTRUCTURE ONLY: see mpcg_oracle.h for scope, the
+ * reference lines each routine follows, and the pinning status.
+ *
+ * Deliberately written as the most literal, loop-per-formula C: dense 7x7
+ * stage blocks, Jacobi eigen-decomposition, textbook Riccati recursion.  It
+ * shares no source with the HIP kernels it checks.
+ */
+#include "mpcg_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NX ORC_NX
+#define NU ORC_NU
+#define NZ ORC_NZ
+#define BIGBOUND 1e15 /* generate_acados_solver.py:17-24 maps +-inf to +-1e15 */
+
+/* acados return codes (acados/utils/types.h) */
+enum { AC_SUCCESS = 0, AC_NAN = 1, AC_MAXITER = 2, AC_MINSTEP = 3, AC_QP_FAILURE = 4 };
+
+/* ------------------------------------------------------------------ */
+/* Glued cubic spline (spline.py:4-86)                                 */
+/* ------------------------------------------------------------------ */
+
+/* value and first two s-derivatives of the sigmoid glue weight
+ * lambda_k(s) = 1 / (1 + exp((s - s_k + 0.02) / 0.1))        (spline.py:37) */
+static void glue_weight(double s, double sk, double *l0, double *l1, double *l2) {
+    double e = exp((s - sk + 0.02) / 0.1);
+    double l = 1.0 / (1.0 + e);
+    *l0 = l;
+    *l1 = -10.0 * l * (1.0 - l);
+    *l2 = 100.0 * l * (1.0 - l) * (1.0 - 2.0 * l);
+}
+
+/* For one axis: G = glued position (spline.py:39-44) and D = glued segment
+ * derivative (spline.py:46-51), each with its first two s-derivatives. */
+static void spline_axis(const orc_problem *pr, const double *p, double s, int axis,
+                        const double (*lam)[3], double G[3], double D[3]) {
+    int M = pr->n_seg;
+    double Pj[ORC_MAX_SEG][4]; /* P, P', P'', P''' of each segment */
+    for (int j = 0; j < M; j++) {
+        const double *c = p + pr->i_spline0 + 9 * j + 4 * axis;
+        double t = s - p[pr->i_spline0 + 9 * j + 8];
+        double a = c[0], b = c[1], cc = c[2], d = c[3];
+        Pj[j][0] = a * t * t * t + b * t * t + cc * t + d;
+        Pj[j][1] = 3.0 * a * t * t + 2.0 * b * t + cc;
+        Pj[j][2] = 6.0 * a * t + 2.0 * b;
+        Pj[j][3] = 6.0 * a;
+    }
+    double V[3] = {Pj[M - 1][0], Pj[M - 1][1], Pj[M - 1][2]};
+    double W[3] = {Pj[M - 1][1], Pj[M - 1][2], Pj[M - 1][3]};
+    for (int k = M - 1; k >= 1; k--) {
+        double l0 = lam[k][0], l1 = lam[k][1], l2 = lam[k][2];
+        const double *A = Pj[k - 1];
+        double nV0 = l0 * A[0] + (1.0 - l0) * V[0];
+        double nV1 = l1 * (A[0] - V[0]) + l0 * A[1] + (1.0 - l0) * V[1];
+        double nV2 = l2 * (A[0] - V[0]) + 2.0 * l1 * (A[1] - V[1]) + l0 * A[2] + (1.0 - l0) * V[2];
+        double nW0 = l0 * A[1] + (1.0 - l0) * W[0];
+        double nW1 = l1 * (A[1] - W[0]) + l0 * A[2] + (1.0 - l0) * W[1];
+        double nW2 = l2 * (A[1] - W[0]) + 2.0 * l1 * (A[2] - W[1]) + l0 * A[3] + (1.0 - l0) * W[2];
+        V[0] = nV0; V[1] = nV1; V[2] = nV2;
+        W[0] = nW0; W[1] = nW1; W[2] = nW2;
+    }
+    memcpy(G, V, sizeof V);
+    memcpy(D, W, sizeof W);
+}
+
+/* ------------------------------------------------------------------ */
+/* Stage cost (solver_definition.py:19-34)                            */
+/* ------------------------------------------------------------------ */
+void orc_stage_cost(const orc_problem *pr, const double *z, const double *p,
+                    double *Lout, double *grad, double *hess) {
+    double a = z[0], w = z[1], x = z[2], y = z[3], v = z[5], s = z[6];
+    double g[NZ] = {0}, H[NZ][NZ];
+    memset(H, 0, sizeof H);
+    double L = 0.0;
+
+    /* MPCBase weights (mpc_base.py:47-60; cost functions as configured in
+     * generate_jackalsimulator_solver.py:47-53) */
+    double wa = p[pr->i_w_acc], ww = p[pr->i_w_ang];
+    double wv = p[pr->i_w_vel], vref = p[pr->i_v_ref];
+    L += wa * a * a;
+    g[0] += 2.0 * wa * a; H[0][0] += 2.0 * wa;
+    L += ww * w * w;
+    g[1] += 2.0 * ww * w; H[1][1] += 2.0 * ww;
+    L += wv * (v - vref) * (v - vref);
+    g[5] += 2.0 * wv * (v - vref); H[5][5] += 2.0 * wv;
+
+    /* Contouring (contouring.py:140-174), stage_idx=1 => no terminal terms */
+    double lam[ORC_MAX_SEG][3];
+    for (int k = 1; k < pr->n_seg; k++)
+        glue_weight(s, p[pr->i_spline0 + 9 * k + 8], &lam[k][0], &lam[k][1], &lam[k][2]);
+    double Gx[3], Dx[3], Gy[3], Dy[3];
+    spline_axis(pr, p, s, 0, (const double (*)[3])lam, Gx, Dx);
+    spline_axis(pr, p, s, 1, (const double (*)[3])lam, Gy, Dy);
+    /* unit tangent t = D/|D| (spline.py:72-77) and its s-derivatives */
+    double r = sqrt(Dx[0] * Dx[0] + Dy[0] * Dy[0]);
+    double tx = Dx[0] / r, ty = Dy[0] / r;
+    double r1 = tx * Dx[1] + ty * Dy[1];
+    double tx1 = (Dx[1] - tx * r1) / r, ty1 = (Dy[1] - ty * r1) / r;
+    double r2 = tx1 * Dx[1] + ty1 * Dy[1] + tx * Dx[2] + ty * Dy[2];
+    double tx2 = (Dx[2] - 2.0 * tx1 * r1 - tx * r2) / r;
+    double ty2 = (Dy[2] - 2.0 * ty1 * r1 - ty * r2) / r;
+    double ex = x - Gx[0], ey = y - Gy[0];
+    double wc = p[pr->i_w_contour], wl = p[pr->i_w_lag];
+
+    /* contour error e_c = ty*ex - tx*ey, lag error e_l = tx*ex + ty*ey (contouring.py:166-167) */
+    double ec = ty * ex - tx * ey;
+    double el = tx * ex + ty * ey;
+    /* gradients over (x, y, s) */
+    double dec[3] = {ty, -tx, ty1 * ex - tx1 * ey - ty * Gx[1] + tx * Gy[1]};
+    double del[3] = {tx, ty, tx1 * ex + ty1 * ey - tx * Gx[1] - ty * Gy[1]};
+    /* second derivatives over (x, y, s) */
+    double hec[3][3] = {{0, 0, ty1}, {0, 0, -tx1},
+                        {ty1, -tx1, ty2 * ex - tx2 * ey - 2.0 * ty1 * Gx[1] + 2.0 * tx1 * Gy[1] - ty * Gx[2] + tx * Gy[2]}};
+    double hel[3][3] = {{0, 0, tx1}, {0, 0, ty1},
+                        {tx1, ty1, tx2 * ex + ty2 * ey - 2.0 * tx1 * Gx[1] - 2.0 * ty1 * Gy[1] - tx * Gx[2] - ty * Gy[2]}};
+    static const int ids[3] = {2, 3, 6};
+    L += wl * el * el;
+    L += wc * ec * ec;
+    for (int i = 0; i < 3; i++) {
+        g[ids[i]] += 2.0 * wl * el * del[i] + 2.0 * wc * ec * dec[i];
+        for (int j = 0; j < 3; j++)
+            H[ids[i]][ids[j]] += 2.0 * wl * (del[i] * del[j] + el * hel[i][j]) +
+                                 2.0 * wc * (dec[i] * dec[j] + ec * hec[i][j]);
+    }
+
+    /* Consistency (consistency_module.py:229-250) */
+    if (pr->i_cons_w >= 0) {
+        double wcn = p[pr->i_cons_w];
+        double dx = x - p[pr->i_prev_x], dy = y - p[pr->i_prev_y];
+        L += wcn * (dx * dx + dy * dy);
+        g[2] += 2.0 * wcn * dx; g[3] += 2.0 * wcn * dy;
+        H[2][2] += 2.0 * wcn; H[3][3] += 2.0 * wcn;
+    }
+    *Lout = L;
+    if (grad) memcpy(grad, g, sizeof g);
+    if (hess) memcpy(hess, H, sizeof H);
+}
+
+/* ------------------------------------------------------------------ */
+/* Constraints h(z) (solver_definition.py:37-49)                      */
+/* ------------------------------------------------------------------ */
+int orc_num_h(const orc_problem *pr) { return pr->n_lin + pr->n_ell; }
+
+void orc_h_bounds(const orc_problem *pr, double *lh, double *uh) {
+    /* guidance_constraints.py:343-353: (-inf, 0]; ellipsoid_constraints.py:421-433: [1, inf) */
+    for (int i = 0; i < pr->n_lin; i++) { lh[i] = -BIGBOUND; uh[i] = 0.0; }
+    for (int j = 0; j < pr->n_ell; j++) { lh[pr->n_lin + j] = 1.0; uh[pr->n_lin + j] = BIGBOUND; }
+}
+
+void orc_stage_constraints(const orc_problem *pr, const double *z, const double *p,
+                           double *h, double *jac, double *hess) {
+    int nh = orc_num_h(pr);
+    double x = z[2], y = z[3], psi = z[4];
+    memset(jac, 0, sizeof(double) * nh * NZ);
+    if (hess) memset(hess, 0, sizeof(double) * nh * NZ * NZ);
+    /* topology halfspaces a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370) */
+    for (int i = 0; i < pr->n_lin; i++) {
+        const double *c = p + pr->i_lin0 + 3 * i;
+        h[i] = c[0] * x + c[1] * y - c[2];
+        jac[i * NZ + 2] = c[0];
+        jac[i * NZ + 3] = c[1];
+    }
+    /* obstacle ellipsoids d' R' D R d >= 1 (ellipsoid_constraints.py:435-489), one disc */
+    double rd = p[pr->i_disc_r], off = p[pr->i_disc_off];
+    double cp = cos(psi), sp = sin(psi);
+    double dxp = -off * sp, dyp = off * cp;       /* d(disc)/dpsi */
+    double dxpp = -off * cp, dypp = -off * sp;    /* d2(disc)/dpsi2 */
+    for (int j = 0; j < pr->n_ell; j++) {
+        const double *o = p + pr->i_ell0 + 7 * j;
+        double chi = sqrt(o[5]);
+        double ra = o[3] * chi + rd + o[6];
+        double rb = o[4] * chi + rd + o[6];
+        double D0 = 1.0 / (ra * ra), D1 = 1.0 / (rb * rb);
+        double c = cos(o[2]), s = sin(o[2]);
+        double M00 = c * c * D0 + s * s * D1;
+        double M01 = -c * s * D0 + s * c * D1;
+        double M11 = s * s * D0 + c * c * D1;
+        double dx = x + off * cp - o[0];
+        double dy = y + off * sp - o[1];
+        double Mdx = M00 * dx + M01 * dy, Mdy = M01 * dx + M11 * dy;
+        int r = pr->n_lin + j;
+        h[r] = dx * Mdx + dy * Mdy;
+        jac[r * NZ + 2] = 2.0 * Mdx;
+        jac[r * NZ + 3] = 2.0 * Mdy;
+        jac[r * NZ + 4] = 2.0 * (Mdx * dxp + Mdy * dyp);
+        if (hess) {
+            double *Hr = hess + (size_t)r * NZ * NZ;
+            Hr[2 * NZ + 2] = 2.0 * M00; Hr[2 * NZ + 3] = 2.0 * M01;
+            Hr[3 * NZ + 2] = 2.0 * M01; Hr[3 * NZ + 3] = 2.0 * M11;
+            double hxp = 2.0 * (M00 * dxp + M01 * dyp);
+            double hyp = 2.0 * (M01 * dxp + M11 * dyp);
+            Hr[2 * NZ + 4] = hxp; Hr[4 * NZ + 2] = hxp;
+            Hr[3 * NZ + 4] = hyp; Hr[4 * NZ + 3] = hyp;
+            Hr[4 * NZ + 4] = 2.0 * (dxp * (M00 * dxp + M01 * dyp) + dyp * (M01 * dxp + M11 * dyp)) +
+                             2.0 * (Mdx * dxpp + Mdy * dypp);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Dynamics (solver_model.py:207-214)                                  */
+/* ------------------------------------------------------------------ */
+void orc_dynamics(const double *z, double *f, double *jac, double *hess) {
+    double a = z[0], w = z[1], psi = z[4], v = z[5];
+    double c = cos(psi), s = sin(psi);
+    f[0] = v * c; f[1] = v * s; f[2] = w; f[3] = a; f[4] = v;
+    if (jac) {
+        memset(jac, 0, sizeof(double) * NX * NZ);
+        jac[0 * NZ + 4] = -v * s; jac[0 * NZ + 5] = c;
+        jac[1 * NZ + 4] = v * c;  jac[1 * NZ + 5] = s;
+        jac[2 * NZ + 1] = 1.0;
+        jac[3 * NZ + 0] = 1.0;
+        jac[4 * NZ + 5] = 1.0;
+    }
+    if (hess) {
+        memset(hess, 0, sizeof(double) * NX * NZ * NZ);
+        hess[0 * NZ * NZ + 4 * NZ + 4] = -v * c;
+        hess[0 * NZ * NZ + 4 * NZ + 5] = -s; hess[0 * NZ * NZ + 5 * NZ + 4] = -s;
+        hess[1 * NZ * NZ + 4 * NZ + 4] = -v * s;
+        hess[1 * NZ * NZ + 4 * NZ + 5] = c; hess[1 * NZ * NZ + 5 * NZ + 4] = c;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* acados ERK (4 stages, rk_steps steps) with forward sensitivities and */
+/* the exact second-order adjoint (generate_acados_solver.py:148-150,   */
+/* hessian_approx EXACT :155)                                           */
+/* ------------------------------------------------------------------ */
+#define ORC_MAX_EVAL 64
+void orc_erk4(const orc_problem *pr, const double *z, double *xnext, double *A, double *B,
+              const double *adj, double *hess) {
+    int ns = pr->rk_steps;
+    double h = pr->dt / ns;
+    double y[NX], S[NX][NZ];
+    static const double cst[4] = {0.0, 0.5, 0.5, 1.0};
+    static const double wgt[4] = {1.0 / 6.0, 2.0 / 6.0, 2.0 / 6.0, 1.0 / 6.0};
+    double W[ORC_MAX_EVAL][NZ];           /* f argument (z-order) of each evaluation */
+    double Se[ORC_MAX_EVAL][NX][NZ];      /* d(state argument)/dz */
+    double Je[ORC_MAX_EVAL][NX][NZ];      /* df/dz' at the argument */
+    for (int i = 0; i < NX; i++) {
+        y[i] = z[NU + i];
+        for (int j = 0; j < NZ; j++) S[i][j] = (j == NU + i) ? 1.0 : 0.0;
+    }
+    int e = 0;
+    for (int st = 0; st < ns; st++) {
+        double k[4][NX], dk[4][NX][NZ];
+        for (int q = 0; q < 4; q++, e++) {
+            /* argument y + c_q h k_{q-1} */
+            W[e][0] = z[0]; W[e][1] = z[1];
+            for (int i = 0; i < NX; i++) {
+                W[e][NU + i] = y[i] + (q ? cst[q] * h * k[q - 1][i] : 0.0);
+                for (int j = 0; j < NZ; j++)
+                    Se[e][i][j] = S[i][j] + (q ? cst[q] * h * dk[q - 1][i][j] : 0.0);
+            }
+            double J[NX * NZ];
+            orc_dynamics(W[e], k[q], J, NULL);
+            for (int i = 0; i < NX; i++)
+                for (int j = 0; j < NZ; j++) Je[e][i][j] = J[i * NZ + j];
+            /* dk = Jx * Se + Ju * [I 0] */
+            for (int i = 0; i < NX; i++)
+                for (int j = 0; j < NZ; j++) {
+                    double acc = (j < NU) ? J[i * NZ + j] : 0.0;
+                    for (int m = 0; m < NX; m++) acc += J[i * NZ + NU + m] * Se[e][m][j];
+                    dk[q][i][j] = acc;
+                }
+        }
+        for (int i = 0; i < NX; i++) {
+            y[i] += h * (wgt[0] * k[0][i] + wgt[1] * k[1][i] + wgt[2] * k[2][i] + wgt[3] * k[3][i]);
+            for (int j = 0; j < NZ; j++)
+                S[i][j] += h * (wgt[0] * dk[0][i][j] + wgt[1] * dk[1][i][j] + wgt[2] * dk[2][i][j] + wgt[3] * dk[3][i][j]);
+        }
+    }
+    for (int i = 0; i < NX; i++) {
+        xnext[i] = y[i];
+        for (int j = 0; j < NX; j++) A[i * NX + j] = S[i][NU + j];
+        for (int j = 0; j < NU; j++) B[i * NU + j] = S[i][j];
+    }
+    if (!adj || !hess) return;
+    /* reverse sweep: ybar = adjoint of the step output; kbar_q = adjoint of k_q */
+    double yb[NX];
+    memcpy(yb, adj, sizeof yb);
+    memset(hess, 0, sizeof(double) * NZ * NZ);
+    for (int st = ns - 1; st >= 0; st--) {
+        double kb[4][NX];
+        int e0 = 4 * st;
+        for (int q = 3; q >= 0; q--) {
+            for (int i = 0; i < NX; i++) kb[q][i] = h * wgt[q] * yb[i];
+            if (q < 3) { /* k_q feeds the argument of k_{q+1} with factor c_{q+1} h */
+                for (int i = 0; i < NX; i++) {
+                    double acc = 0.0;
+                    for (int m = 0; m < NX; m++) acc += Je[e0 + q + 1][m][NU + i] * kb[q + 1][m];
+                    kb[q][i] += cst[q + 1] * h * acc;
+                }
+            }
+        }
+        double ybn[NX];
+        for (int i = 0; i < NX; i++) {
+            double acc = yb[i];
+            for (int q = 0; q < 4; q++)
+                for (int m = 0; m < NX; m++) acc += Je[e0 + q][m][NU + i] * kb[q][m];
+            ybn[i] = acc;
+        }
+        /* second-order terms: sum_q We' Hess(kbar_q' f) We, We = d[u; y_arg]/dz */
+        for (int q = 0; q < 4; q++) {
+            int ee = e0 + q;
+            double Hf[NX * NZ * NZ], f[NX], Hm[NZ][NZ], Wm[NZ][NZ];
+            orc_dynamics(W[ee], f, NULL, Hf);
+            for (int i = 0; i < NZ; i++)
+                for (int j = 0; j < NZ; j++) {
+                    double acc = 0.0;
+                    for (int m = 0; m < NX; m++) acc += kb[q][m] * Hf[m * NZ * NZ + i * NZ + j];
+                    Hm[i][j] = acc;
+                }
+            for (int i = 0; i < NZ; i++)
+                for (int j = 0; j < NZ; j++)
+                    Wm[i][j] = (i < NU) ? (i == j ? 1.0 : 0.0) : Se[ee][i - NU][j];
+            for (int i = 0; i < NZ; i++)
+                for (int j = 0; j < NZ; j++) {
+                    double acc = 0.0;
+                    for (int m = 0; m < NZ; m++)
+                        for (int n = 0; n < NZ; n++) acc += Wm[m][i] * Hm[m][n] * Wm[n][j];
+                    hess[i * NZ + j] += acc;
+                }
+        }
+        memcpy(yb, ybn, sizeof yb);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* MIRROR regularisation (regularize_method "MIRROR",                  */
+/* generate_acados_solver.py:157): H = V f(D) V', f(d)=eps if |d|<=eps  */
+/* else |d|.  Eigen-decomposition by cyclic Jacobi.                     */
+/* ------------------------------------------------------------------ */
+void orc_mirror(int n, double *H, double eps) {
+    double a[NZ][NZ], V[NZ][NZ], d[NZ];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            a[i][j] = 0.5 * (H[i * n + j] + H[j * n + i]);
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double off = 0.0, dia = 0.0;
+        for (int i = 0; i < n; i++) {
+            dia += a[i][i] * a[i][i];
+            for (int j = i + 1; j < n; j++) off += a[i][j] * a[i][j];
+        }
+        if (off <= 1e-32 * dia || off < 1e-300) break;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                double apq = a[p][q];
+                if (fabs(apq) < 1e-300) continue;
+                double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+                double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; k++) { /* columns p, q */
+                    double akp = a[k][p], akq = a[k][q];
+                    a[k][p] = c * akp - s * akq;
+                    a[k][q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; k++) { /* rows p, q */
+                    double apk = a[p][k], aqk = a[q][k];
+                    a[p][k] = c * apk - s * aqk;
+                    a[q][k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; k++) {
+                    double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = c * vkp - s * vkq;
+                    V[k][q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < n; i++) {
+        double di = a[i][i];
+        if (di >= -eps && di <= eps) di = eps;
+        else if (di < 0.0) di = -di;
+        d[i] = di;
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double acc = 0.0;
+            for (int k = 0; k < n; k++) acc += V[i][k] * d[k] * V[j][k];
+            H[i * n + j] = acc;
+        }
+}
+
+/* ------------------------------------------------------------------ */
+/* OCP-QP: Riccati-based Mehrotra primal-dual interior point            */
+/* (PARTIAL_CONDENSING_HPIPM with cond_N = N, qp_tol 1e-5, iter_max 50:  */
+/* generate_acados_solver.py:162-173).  Inequalities D z <= d, one      */
+/* sided; +-1e15 bounds are dropped.  x0 is eliminated (fixed).         */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    double H[NZ][NZ], g[NZ];
+    double A[NX][NX], B[NX][NU], b[NX];
+    int ni;
+    double (*D)[NZ];
+    double *d, *t, *lam, *dt, *dl, *dt_aff, *dl_aff, *rin, *rc;
+    int *hrow; /* >=0: index of the h-row this inequality came from (sign in hsgn) */
+    int *hsgn;
+    /* Riccati storage */
+    double L[NU][NU], Y[NU][NX], P[NX][NX], p[NX], y[NU];
+    double Hh[NZ][NZ], q[NZ];
+    double dz[NZ], ddz[NZ], pi[NX], pin[NX];
+} qp_stage;
+
+typedef struct {
+    int N;
+    qp_stage *st; /* N+1 */
+} qp_ws;
+
+/* stationarity residual of stage k on its free variables */
+static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *mu, int *mtot) {
+    int N = w->N;
+    double s_max = 0.0, e_max = 0.0, i_max = 0.0, comp = 0.0;
+    int m = 0;
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w->st[k];
+        double r[NZ];
+        for (int i = 0; i < NZ; i++) {
+            double acc = S->g[i];
+            for (int j = 0; j < NZ; j++) acc += S->H[i][j] * S->dz[j];
+            r[i] = acc;
+        }
+        if (k < N) {
+            for (int i = 0; i < NZ; i++) {
+                double acc = 0.0;
+                for (int m2 = 0; m2 < NX; m2++)
+                    acc += (i < NU ? S->B[m2][i] : S->A[m2][i - NU]) * S->pi[m2];
+                r[i] += acc;
+            }
+        }
+        if (k > 0)
+            for (int i = 0; i < NX; i++) r[NU + i] -= w->st[k - 1].pi[i];
+        for (int c = 0; c < S->ni; c++) {
+            for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * S->lam[c];
+            double acc = S->t[c] - S->d[c];
+            for (int i = 0; i < NZ; i++) acc += S->D[c][i] * S->dz[i];
+            S->rin[c] = acc;
+            if (fabs(acc) > i_max) i_max = fabs(acc);
+            comp += S->lam[c] * S->t[c];
+            m++;
+        }
+        int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
+        for (int i = i0; i < i1; i++)
+            if (fabs(r[i]) > s_max) s_max = fabs(r[i]);
+        if (k < N) {
+            qp_stage *S1 = &w->st[k + 1];
+            for (int i = 0; i < NX; i++) {
+                double acc = S->b[i] - S1->dz[NU + i];
+                for (int j = 0; j < NX; j++) acc += S->A[i][j] * S->dz[NU + j];
+                for (int j = 0; j < NU; j++) acc += S->B[i][j] * S->dz[j];
+                if (fabs(acc) > e_max) e_max = fabs(acc);
+            }
+        }
+    }
+    *rs = s_max; *re = e_max; *ri = i_max;
+    *mtot = m;
+    *mu = m ? comp / m : 0.0;
+}
+
+/* dynamics residual r_k = A dx_k + B du_k + b_k - dx_{k+1} */
+static void dyn_res(qp_ws *w, int k, double r[NX]) {
+    qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
+    for (int i = 0; i < NX; i++) {
+        double acc = S->b[i] - S1->dz[NU + i];
+        for (int j = 0; j < NX; j++) acc += S->A[i][j] * S->dz[NU + j];
+        for (int j = 0; j < NU; j++) acc += S->B[i][j] * S->dz[j];
+        r[i] = acc;
+    }
+}
+
+/* Riccati factorisation of the barrier-augmented Hessians Hh. returns 0 ok */
+static int riccati_factor(qp_ws *w) {
+    int N = w->N;
+    qp_stage *SN = &w->st[N];
+    for (int i = 0; i < NX; i++)
+        for (int j = 0; j < NX; j++) SN->P[i][j] = SN->Hh[NU + i][NU + j];
+    for (int k = N - 1; k >= 0; k--) {
+        qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
+        double F[NX][NZ], PF[NX][NZ], M[NZ][NZ];
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NZ; j++) F[i][j] = (j < NU) ? S->B[i][j] : S->A[i][j - NU];
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NZ; j++) {
+                double acc = 0.0;
+                for (int m = 0; m < NX; m++) acc += S1->P[i][m] * F[m][j];
+                PF[i][j] = acc;
+            }
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NZ; j++) {
+                double acc = S->Hh[i][j];
+                for (int m = 0; m < NX; m++) acc += F[m][i] * PF[m][j];
+                M[i][j] = acc;
+            }
+        /* Cholesky of Muu */
+        double l00 = M[0][0];
+        if (!(l00 > 0.0)) return -1;
+        l00 = sqrt(l00);
+        double l10 = M[1][0] / l00;
+        double l11 = M[1][1] - l10 * l10;
+        if (!(l11 > 0.0)) return -1;
+        l11 = sqrt(l11);
+        S->L[0][0] = l00; S->L[0][1] = 0.0; S->L[1][0] = l10; S->L[1][1] = l11;
+        /* Y = L^{-1} Mux */
+        for (int j = 0; j < NX; j++) {
+            double y0 = M[0][NU + j] / l00;
+            double y1 = (M[1][NU + j] - l10 * y0) / l11;
+            S->Y[0][j] = y0; S->Y[1][j] = y1;
+        }
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++)
+                S->P[i][j] = M[NU + i][NU + j] - S->Y[0][i] * S->Y[0][j] - S->Y[1][i] * S->Y[1][j];
+    }
+    return 0;
+}
+
+/* vector pass + forward substitution for gradient q (in S->q) and the
+ * current dynamics residuals; writes ddz (step) and pin (new dynamics
+ * multipliers) */
+static void riccati_solve(qp_ws *w) {
+    int N = w->N;
+    double r[ORC_MAX_N][NX];
+    for (int k = 0; k < N; k++) dyn_res(w, k, r[k]);
+    qp_stage *SN = &w->st[N];
+    for (int i = 0; i < NX; i++) SN->p[i] = SN->q[NU + i];
+    for (int k = N - 1; k >= 0; k--) {
+        qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
+        double v[NX], m[NZ];
+        for (int i = 0; i < NX; i++) {
+            double acc = S1->p[i];
+            for (int j = 0; j < NX; j++) acc += S1->P[i][j] * r[k][j];
+            v[i] = acc;
+        }
+        for (int i = 0; i < NZ; i++) {
+            double acc = S->q[i];
+            for (int j = 0; j < NX; j++) acc += (i < NU ? S->B[j][i] : S->A[j][i - NU]) * v[j];
+            m[i] = acc;
+        }
+        double y0 = m[0] / S->L[0][0];
+        double y1 = (m[1] - S->L[1][0] * y0) / S->L[1][1];
+        S->y[0] = y0; S->y[1] = y1;
+        for (int i = 0; i < NX; i++) S->p[i] = m[NU + i] - S->Y[0][i] * y0 - S->Y[1][i] * y1;
+    }
+    /* forward */
+    double dx[NX] = {0};
+    for (int k = 0; k < N; k++) {
+        qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
+        /* du = -L^{-T} (Y dx + y) */
+        double c0 = S->y[0], c1 = S->y[1];
+        for (int j = 0; j < NX; j++) { c0 += S->Y[0][j] * dx[j]; c1 += S->Y[1][j] * dx[j]; }
+        /* L^T du = -c  => [l00 l10; 0 l11] du = -c */
+        double du1 = -c1 / S->L[1][1];
+        double du0 = (-c0 - S->L[1][0] * du1) / S->L[0][0];
+        S->ddz[0] = du0; S->ddz[1] = du1;
+        for (int i = 0; i < NX; i++) S->ddz[NU + i] = (k == 0) ? 0.0 : dx[i];
+        double dxn[NX];
+        for (int i = 0; i < NX; i++) {
+            double acc = r[k][i] + S->B[i][0] * du0 + S->B[i][1] * du1;
+            for (int j = 0; j < NX; j++) acc += S->A[i][j] * dx[j];
+            dxn[i] = acc;
+        }
+        for (int i = 0; i < NX; i++) {
+            double acc = S1->p[i];
+            for (int j = 0; j < NX; j++) acc += S1->P[i][j] * dxn[j];
+            S->pin[i] = acc;
+        }
+        memcpy(dx, dxn, sizeof dx);
+    }
+    SN->ddz[0] = SN->ddz[1] = 0.0;
+    for (int i = 0; i < NX; i++) SN->ddz[NU + i] = dx[i];
+}
+
+/* gradient of the Newton system for complementarity targets rc */
+static void build_q(qp_ws *w) {
+    for (int k = 0; k <= w->N; k++) {
+        qp_stage *S = &w->st[k];
+        for (int i = 0; i < NZ; i++) {
+            double acc = S->g[i];
+            for (int j = 0; j < NZ; j++) acc += S->H[i][j] * S->dz[j];
+            S->q[i] = acc;
+        }
+        for (int c = 0; c < S->ni; c++) {
+            double coef = S->lam[c] + (S->lam[c] * S->rin[c] - S->rc[c]) / S->t[c];
+            for (int i = 0; i < NZ; i++) S->q[i] += S->D[c][i] * coef;
+        }
+    }
+}
+
+static void ineq_steps(qp_ws *w, double *dtv_unused) {
+    (void)dtv_unused;
+    for (int k = 0; k <= w->N; k++) {
+        qp_stage *S = &w->st[k];
+        for (int c = 0; c < S->ni; c++) {
+            double acc = 0.0;
+            for (int i = 0; i < NZ; i++) acc += S->D[c][i] * S->ddz[i];
+            S->dt[c] = -S->rin[c] - acc;
+            S->dl[c] = -(S->rc[c] + S->lam[c] * S->dt[c]) / S->t[c];
+        }
+    }
+}
+
+static double max_step(qp_ws *w) {
+    double amax = 1e300;
+    for (int k = 0; k <= w->N; k++) {
+        qp_stage *S = &w->st[k];
+        for (int c = 0; c < S->ni; c++) {
+            if (S->dt[c] < 0.0) { double a = -S->t[c] / S->dt[c]; if (a < amax) amax = a; }
+            if (S->dl[c] < 0.0) { double a = -S->lam[c] / S->dl[c]; if (a < amax) amax = a; }
+        }
+    }
+    return amax;
+}
+
+static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters) {
+    int N = w->N;
+    /* cold start */
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w->st[k];
+        for (int i = 0; i < NZ; i++)
+            if (!(k == 0 && i >= NU)) S->dz[i] = 0.0; /* x0 part stays fixed */
+        for (int i = 0; i < NX; i++) S->pi[i] = 0.0;
+        for (int c = 0; c < S->ni; c++) {
+            double s = S->d[c];
+            for (int i = 0; i < NZ; i++) s -= S->D[c][i] * S->dz[i];
+            S->t[c] = s > pr->qp_thr0 ? s : pr->qp_thr0;
+            S->lam[c] = pr->qp_mu0 / S->t[c];
+        }
+    }
+    int status = AC_MAXITER;
+    int it;
+    for (it = 0;; it++) {
+        double rs, re, ri, mu;
+        int m;
+        qp_residuals(w, &rs, &re, &ri, &mu, &m);
+        /* non-finite or diverged (infeasible QP: duals blow up) -> NaN status */
+        if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { status = AC_NAN; break; }
+        if (getenv("ORC_DEBUG")) fprintf(stderr, "  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", it, rs, re, ri, mu);
+        if (rs < pr->qp_tol && re < pr->qp_tol && ri < pr->qp_tol && mu < pr->qp_tol) { status = AC_SUCCESS; break; }
+        if (it >= pr->qp_iter_max) { status = AC_MAXITER; break; }
+        /* barrier-augmented Hessian */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            memcpy(S->Hh, S->H, sizeof S->H);
+            for (int c = 0; c < S->ni; c++) {
+                double wc = S->lam[c] / S->t[c];
+                for (int i = 0; i < NZ; i++) {
+                    if (S->D[c][i] == 0.0) continue;
+                    for (int j = 0; j < NZ; j++) S->Hh[i][j] += S->D[c][i] * wc * S->D[c][j];
+                }
+            }
+        }
+        if (riccati_factor(w)) { status = AC_NAN; break; }
+        /* predictor */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int c = 0; c < S->ni; c++) S->rc[c] = S->lam[c] * S->t[c];
+        }
+        build_q(w);
+        riccati_solve(w);
+        ineq_steps(w, NULL);
+        double aa = max_step(w);
+        if (aa > 1.0) aa = 1.0;
+        double comp_aff = 0.0;
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int c = 0; c < S->ni; c++) {
+                comp_aff += (S->lam[c] + aa * S->dl[c]) * (S->t[c] + aa * S->dt[c]);
+                S->dt_aff[c] = S->dt[c];
+                S->dl_aff[c] = S->dl[c];
+            }
+        }
+        double mu_aff = comp_aff / m;
+        double sig = mu_aff / mu;
+        if (sig > 1.0) sig = 1.0;
+        sig = sig * sig * sig;
+        /* corrector */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int c = 0; c < S->ni; c++)
+                S->rc[c] = S->lam[c] * S->t[c] + S->dl_aff[c] * S->dt_aff[c] - sig * mu;
+        }
+        build_q(w);
+        riccati_solve(w);
+        ineq_steps(w, NULL);
+        double alpha = 0.995 * max_step(w);
+        if (alpha > 1.0) alpha = 1.0;
+        if (alpha < 1e-12) { status = AC_MINSTEP; it++; break; }
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int i = 0; i < NZ; i++) S->dz[i] += alpha * S->ddz[i];
+            if (k < N)
+                for (int i = 0; i < NX; i++) S->pi[i] += alpha * (S->pin[i] - S->pi[i]);
+            for (int c = 0; c < S->ni; c++) {
+                S->t[c] += alpha * S->dt[c];
+                S->lam[c] += alpha * S->dl[c];
+            }
+        }
+    }
+    *iters = it;
+    return status;
+}
+
+/* ------------------------------------------------------------------ */
+/* Solver::solve() (acados_solver_interface.cpp:311-429)              */
+/* ------------------------------------------------------------------ */
+int orc_solve(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
+              double *xtraj, double *utraj, orc_info *info) {
+    int N = pr->N, npar = pr->npar;
+    int nh = orc_num_h(pr);
+    int maxi = 2 * NZ + 2 * nh;
+    double lh[ORC_MAX_LIN + ORC_MAX_ELL], uh[ORC_MAX_LIN + ORC_MAX_ELL];
+    orc_h_bounds(pr, lh, uh);
+
+    qp_ws w;
+    w.N = N;
+    w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
+    size_t nrow = (size_t)(N + 1) * maxi;
+    double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));
+    double *dbl = (double *)calloc(nrow * 9, sizeof(double));
+    int *ibl = (int *)calloc(nrow * 2, sizeof(int));
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w.st[k];
+        size_t o = (size_t)k * maxi;
+        S->D = Dall + o;
+        S->d = dbl + o; S->t = dbl + nrow + o; S->lam = dbl + 2 * nrow + o;
+        S->dt = dbl + 3 * nrow + o; S->dl = dbl + 4 * nrow + o; S->dt_aff = dbl + 5 * nrow + o;
+        S->dl_aff = dbl + 6 * nrow + o; S->rin = dbl + 7 * nrow + o; S->rc = dbl + 8 * nrow + o;
+        S->hrow = ibl + o; S->hsgn = ibl + nrow + o;
+    }
+    /* NLP iterate: z_k = [u_k; x_k] from the warm start (loadWarmstart, :499-509);
+     * NLP multipliers start at zero (fresh capsule). */
+    double (*z)[NZ] = (double (*)[NZ])calloc(N + 1, sizeof(double[NZ]));
+    double (*pi)[NX] = (double (*)[NX])calloc(N + 1, sizeof(double[NX]));
+    double *lamh = (double *)calloc((size_t)(N + 1) * 2 * nh, sizeof(double)); /* [k][2*i+side] */
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < NZ; i++) z[k][i] = warm[k * NZ + i];
+    for (int i = 0; i < NU; i++) z[N][i] = 0.0;
+
+    double h[ORC_MAX_LIN + ORC_MAX_ELL], jac[(ORC_MAX_LIN + ORC_MAX_ELL) * NZ];
+    double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
+    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0;
+    double res_eq = 0.0;
+
+    for (int it = 0; it < pr->sqp_iters; it++) {
+        /* ---- linearise at z (preparation phase) ---- */
+        res_eq = 0.0;
+        for (int k = 0; k < N; k++) {
+            qp_stage *S = &w.st[k];
+            const double *p = params + (size_t)k * npar;
+            double L, g[NZ], Hc[NZ * NZ], Hd[NZ * NZ], xn[NX], A[NX * NX], B[NX * NU];
+            orc_stage_cost(pr, z[k], p, &L, g, Hc);
+            orc_erk4(pr, z[k], xn, A, B, pi[k], Hd);
+            for (int i = 0; i < NZ; i++) {
+                S->g[i] = g[i];
+                for (int j = 0; j < NZ; j++) S->H[i][j] = Hc[i * NZ + j] + Hd[i * NZ + j];
+            }
+            for (int i = 0; i < NX; i++) {
+                S->b[i] = xn[i] - z[k + 1][NU + i];
+                if (fabs(S->b[i]) > res_eq) res_eq = fabs(S->b[i]);
+                for (int j = 0; j < NX; j++) S->A[i][j] = A[i * NX + j];
+                for (int j = 0; j < NU; j++) S->B[i][j] = B[i * NU + j];
+            }
+            int ni = 0;
+            /* input bounds (idxbu = all, :104-107) */
+            for (int i = 0; i < NU; i++) {
+                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = -1.0;
+                S->d[ni] = z[k][i] - pr->lbu[i]; S->hrow[ni] = -1; ni++;
+                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = 1.0;
+                S->d[ni] = pr->ubu[i] - z[k][i]; S->hrow[ni] = -1; ni++;
+            }
+            if (k >= 1) {
+                /* state bounds on stages 1..N-1 (idxbx = all, :100-102) */
+                for (int i = 0; i < NX; i++) {
+                    memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = -1.0;
+                    S->d[ni] = z[k][NU + i] - pr->lbx[i]; S->hrow[ni] = -1; ni++;
+                    memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = 1.0;
+                    S->d[ni] = pr->ubx[i] - z[k][NU + i]; S->hrow[ni] = -1; ni++;
+                }
+                /* nonlinear constraints h, linearised; Hessian weighted by the
+                 * NLP multipliers (exact Hessian of the Lagrangian) */
+                orc_stage_constraints(pr, z[k], p, h, jac, hh);
+                for (int r = 0; r < nh; r++) {
+                    double wgt = lamh[(size_t)k * 2 * nh + 2 * r + 1] - lamh[(size_t)k * 2 * nh + 2 * r + 0];
+                    if (wgt != 0.0)
+                        for (int i = 0; i < NZ; i++)
+                            for (int j = 0; j < NZ; j++) S->H[i][j] += wgt * hh[(size_t)r * NZ * NZ + i * NZ + j];
+                    if (uh[r] < BIGBOUND) {
+                        for (int i = 0; i < NZ; i++) S->D[ni][i] = jac[r * NZ + i];
+                        S->d[ni] = uh[r] - h[r]; S->hrow[ni] = r; S->hsgn[ni] = 1; ni++;
+                    }
+                    if (lh[r] > -BIGBOUND) {
+                        for (int i = 0; i < NZ; i++) S->D[ni][i] = -jac[r * NZ + i];
+                        S->d[ni] = h[r] - lh[r]; S->hrow[ni] = r; S->hsgn[ni] = 0; ni++;
+                    }
+                }
+            }
+            S->ni = ni;
+            double Hf[NZ * NZ];
+            for (int i = 0; i < NZ; i++)
+                for (int j = 0; j < NZ; j++) Hf[i * NZ + j] = S->H[i][j];
+            orc_mirror(NZ, Hf, pr->reg_eps);
+            for (int i = 0; i < NZ; i++)
+                for (int j = 0; j < NZ; j++) S->H[i][j] = Hf[i * NZ + j];
+        }
+        /* terminal stage: no cost (cost_type_e default), no constraints,
+         * zero Hessian mirrored to eps*I */
+        {
+            qp_stage *S = &w.st[N];
+            memset(S->H, 0, sizeof S->H);
+            memset(S->g, 0, sizeof S->g);
+            double Hx[NX * NX] = {0};
+            orc_mirror(NX, Hx, pr->reg_eps);
+            for (int i = 0; i < NX; i++)
+                for (int j = 0; j < NX; j++) S->H[NU + i][NU + j] = Hx[i * NX + j];
+            S->ni = 0;
+        }
+        /* x0 elimination: lbx_0 = ubx_0 = xinit (:349-350) */
+        for (int i = 0; i < NX; i++) w.st[0].dz[NU + i] = xinit[i] - z[0][NU + i];
+
+        /* ---- feedback phase: QP ---- */
+        int qit = 0;
+        qp_status = qp_solve(pr, &w, &qit);
+        qp_iter_total += qit;
+        sqp_iter++;
+        if (qp_status != AC_SUCCESS && qp_status != AC_MAXITER) {
+            acados_status = AC_QP_FAILURE;
+            break;
+        }
+        /* FIXED_STEP full step on primal and multipliers */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w.st[k];
+            for (int i = 0; i < NZ; i++) z[k][i] += S->dz[i];
+            if (k < N) memcpy(pi[k], S->pi, sizeof(double) * NX);
+            for (int r = 0; r < 2 * nh; r++) lamh[(size_t)k * 2 * nh + r] = 0.0;
+            for (int c = 0; c < S->ni; c++)
+                if (S->hrow[c] >= 0) lamh[(size_t)k * 2 * nh + 2 * S->hrow[c] + S->hsgn[c]] = S->lam[c];
+        }
+        for (int i = 0; i < NU; i++) z[N][i] = 0.0;
+        acados_status = AC_SUCCESS;
+        /* acados_solver_interface.cpp:330: break when the QP did not succeed */
+        if (qp_status != AC_SUCCESS) break;
+    }
+
+    double pobj = 0.0;
+    for (int k = 0; k < N; k++) {
+        double L;
+        orc_stage_cost(pr, z[k], params + (size_t)k * npar, &L, NULL, NULL);
+        pobj += L;
+    }
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < NX; i++) xtraj[k * NX + i] = z[k][NU + i];
+    for (int k = 0; k < N; k++)
+        for (int i = 0; i < NU; i++) utraj[k * NU + i] = z[k][i];
+
+    int exit_code = acados_status;
+    if (res_eq > pr->res_eq_fail && exit_code == AC_SUCCESS) exit_code = AC_QP_FAILURE;
+    if (exit_code == AC_SUCCESS) exit_code = 1;
+    else if (exit_code == 1) exit_code = 0;
+    if (info) {
+        info->sqp_iter = sqp_iter;
+        info->qp_iter_total = qp_iter_total;
+        info->qp_status = qp_status;
+        info->res_eq = res_eq;
+        info->pobj = pobj;
+    }
+    free(hh); free(lamh); free(pi); free(z);
+    free(ibl); free(dbl); free(Dall); free(w.st);
+    return exit_code;
+}
+
+void orc_solve_batch(const orc_problem *pr, int batch, const double *params, const double *warm,
+                     const double *xinit, double *xtraj, double *utraj, double *pobj,
+                     int *status, int *qp_iters, int nthreads) {
+    int N = pr->N;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+#endif
+    for (int b = 0; b < batch; b++) {
+        orc_info info;
+        status[b] = orc_solve(pr, params + (size_t)b * N * pr->npar, warm + (size_t)b * (N + 1) * NZ,
+                              xinit + (size_t)b * NX, xtraj + (size_t)b * (N + 1) * NX,
+                              utraj + (size_t)b * N * NU, &info);
+        pobj[b] = info.pobj;
+        if (qp_iters) qp_iters[b] = info.qp_iter_total;
+    }
+    (void)nthreads;
+}

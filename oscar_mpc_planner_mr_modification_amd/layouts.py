@@ -1,0 +1,177 @@
+"""Parameter layouts: the horizon-major `all_parameters[k*npar + idx]` map.
+
+Mirrors the reference's `define_parameters` (solver_generator/solver_definition.py:5-16):
+objective modules first, then constraint modules, each appending its
+parameters in declaration order, duplicates skipped (util/parameters.py:187-217).
+The module stacks are the ones the reference's generator scripts build:
+
+* ``tmpc``     — configuration_tmpc_consistency_cost
+                 (mpc_planner_jackalsimulator/scripts/generate_jackalsimulator_solver.py:37-59,107-116):
+                 MPCBase(a, w, v) + Contouring [+ Consistency] + GuidanceConstraints(Ellipsoid)
+* ``lmpcc``    — configuration_basic (same file :62-67): MPCBase + Contouring + Ellipsoid
+
+The resulting maps are checked against the reference's own maps in
+tests/golden/parameter_maps.json.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+# bounds of ContouringSecondOrderUnicycleModel (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
+UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -12.566370614359172, -0.01, -1.0)
+UNICYCLE_UB = (2.0, 0.8, 2000.0, 2000.0, 12.566370614359172, 3.0, 10000.0)
+UNICYCLE_STATES = ("x", "y", "psi", "v", "spline")
+UNICYCLE_INPUTS = ("a", "w")
+
+
+class _Params:
+    """Same add() semantics as util/parameters.py:187-217 (name -> next index,
+    bundle -> list of indices)."""
+
+    def __init__(self):
+        self.map: dict[str, int] = {}
+        self.bundles: dict[str, list[int]] = {}
+
+    def add(self, name: str, bundle: str | None = None):
+        if name in self.map:
+            return
+        idx = len(self.map)
+        self.map[name] = idx
+        self.bundles.setdefault(bundle or name, []).append(idx)
+
+
+def _mpc_base(p: _Params):
+    # weigh_variable a/acceleration, w/angular_velocity, v/[velocity, reference_velocity]
+    for n in ("acceleration", "angular_velocity", "velocity", "reference_velocity"):
+        p.add(n)
+
+
+def _contouring(p: _Params, num_segments: int):
+    # contouring.py:114-138
+    p.add("contour")
+    p.add("lag")
+    if "velocity" not in p.map:
+        p.add("velocity")
+        p.add("reference_velocity")
+    p.add("terminal_angle")
+    p.add("terminal_contouring")
+    for i in range(num_segments):
+        for ax in ("x", "y"):
+            for c in ("a", "b", "c", "d"):
+                p.add(f"spline_{ax}{i}_{c}", f"spline_{ax}_{c}")
+        p.add(f"spline{i}_start", "spline_start")
+
+
+def _consistency(p: _Params):
+    # consistency_module.py:220-227
+    p.add("consistency_weight")
+    p.add("prev_traj_x")
+    p.add("prev_traj_y")
+
+
+def _guidance_linear(p: _Params, n: int):
+    # guidance_constraints.py:333-338
+    for i in range(n):
+        p.add(f"lin_constraint_{i}_a1", "lin_constraint_a1")
+        p.add(f"lin_constraint_{i}_a2", "lin_constraint_a2")
+        p.add(f"lin_constraint_{i}_b", "lin_constraint_b")
+
+
+def _ellipsoid(p: _Params, n_discs: int, n_obs: int):
+    # ellipsoid_constraints.py:406-419
+    p.add("ego_disc_radius")
+    for d in range(n_discs):
+        p.add(f"ego_disc_{d}_offset", "ego_disc_offset")
+    for j in range(n_obs):
+        for f in ("x", "y", "psi", "major", "minor", "chi", "r"):
+            p.add(f"ellipsoid_obst_{j}_{f}", f"ellipsoid_obst_{f}")
+
+
+@dataclass
+class Layout:
+    """Everything the kernels need to find a parameter by meaning."""
+    name: str
+    N: int
+    max_obstacles: int
+    n_lin: int
+    n_ell: int
+    n_seg: int = 5
+    consistency: bool = True
+    dt: float = 0.2
+    rk_steps: int = 3
+    sqp_iters: int = 10
+    pmap: dict = field(default_factory=dict)
+    bundles: dict = field(default_factory=dict)
+
+    @property
+    def npar(self) -> int:
+        return len(self.pmap)
+
+    @property
+    def nx(self) -> int:
+        return 5
+
+    @property
+    def nu(self) -> int:
+        return 2
+
+    @property
+    def nvar(self) -> int:
+        return 7
+
+    @property
+    def nh(self) -> int:
+        return self.n_lin + self.n_ell
+
+    def idx(self, name: str) -> int:
+        return self.pmap.get(name, -1)
+
+    def index_struct(self) -> dict:
+        """Base indices consumed by the C ABI (include/mpcg.h, mpcg_problem)."""
+        g = self.idx
+        return dict(
+            i_w_acc=g("acceleration"), i_w_ang=g("angular_velocity"), i_w_vel=g("velocity"),
+            i_v_ref=g("reference_velocity"), i_w_contour=g("contour"), i_w_lag=g("lag"),
+            i_spline0=g("spline_x0_a"), i_cons_w=g("consistency_weight"),
+            i_prev_x=g("prev_traj_x"), i_prev_y=g("prev_traj_y"),
+            i_lin0=g("lin_constraint_0_a1") if self.n_lin else -1,
+            i_disc_r=g("ego_disc_radius"), i_disc_off=g("ego_disc_0_offset"),
+            i_ell0=g("ellipsoid_obst_0_x") if self.n_ell else -1,
+        )
+
+
+def tmpc_layout(N: int = 20, max_obstacles: int = 8, consistency: bool = True,
+                num_segments: int = 5, add_halfspaces: int = 0, name: str | None = None) -> Layout:
+    p = _Params()
+    _mpc_base(p)
+    _contouring(p, num_segments)
+    if consistency:
+        _consistency(p)
+    n_lin = max_obstacles + add_halfspaces
+    _guidance_linear(p, n_lin)
+    _ellipsoid(p, 1, max_obstacles)
+    return Layout(name=name or f"tmpc_N{N}_obs{max_obstacles}", N=N, max_obstacles=max_obstacles,
+                  n_lin=n_lin, n_ell=max_obstacles, n_seg=num_segments, consistency=consistency,
+                  pmap=p.map, bundles=p.bundles)
+
+
+def lmpcc_layout(N: int = 20, max_obstacles: int = 4, num_segments: int = 5) -> Layout:
+    p = _Params()
+    _mpc_base(p)
+    _contouring(p, num_segments)
+    _ellipsoid(p, 1, max_obstacles)
+    return Layout(name=f"lmpcc_N{N}_obs{max_obstacles}", N=N, max_obstacles=max_obstacles,
+                  n_lin=0, n_ell=max_obstacles, n_seg=num_segments, consistency=False,
+                  pmap=p.map, bundles=p.bundles)
+
+
+# BASELINE.json configs on the unicycle T-MPC problem
+def config_layout(cfg: str) -> Layout:
+    cfg = cfg.upper()
+    if cfg == "C1":
+        return tmpc_layout(N=20, max_obstacles=4, name="C1")
+    if cfg == "C2":
+        return tmpc_layout(N=20, max_obstacles=8, name="C2")
+    if cfg == "C4":
+        return tmpc_layout(N=30, max_obstacles=12, name="C4")
+    raise KeyError(f"config {cfg} has no unicycle layout (C3/C5 are later rows of SURVEY §8f)")

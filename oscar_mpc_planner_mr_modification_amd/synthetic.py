@@ -1,0 +1,262 @@
+"""Seeded synthetic scenes for the batched T-MPC++ solve.
+
+One scene = one control step of `Planner::solveMPC` on the jackal T-MPC
+problem: a 5-segment reference path, the ego state, `n_obs` constant-velocity
+obstacles and G = n_guided + 1 planners (the guided ones plus the T-MPC++
+non-guided one).  For every (scene, planner) pair this module writes exactly
+what the reference's host-side modules write before `Solver::solve()`:
+
+* weights + spline segments for every stage      (mpc_base.cpp:23-35, contouring.cpp:52-126)
+* topology halfspaces from the guess trajectory    (linearized_constraints.cpp:49-128, 150-189;
+  radius 1e-3 + robot_radius because `_use_guidance`, robot centre, no disc;
+  the Douglas-Rachford projection (:130-148, external ros_tools) is omitted)
+* stage-0 dummies                                   (linearized_constraints.cpp:155-166,
+                                                     ellipsoid_constraints.cpp:42-56)
+* obstacle ellipsoids, stage k uses prediction k-1 (ellipsoid_constraints.cpp:61-86)
+* consistency parameters on stages 1..N-2           (guidance_constraints.cpp:986-1023)
+* warm start: braking for the non-guided planner    (acados_solver_interface.cpp:528-567)
+  and guidance-initialised x, y, psi, v on k=1..N-1 for the guided ones
+  (guidance_constraints.cpp:546-570), a/w/spline from the braking warm start.
+
+Seeds: scene i uses `seed + i` (default seed 20251212), so any sub-range of a
+batch (e.g. one GPU's shard) regenerates bit-identically.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .layouts import Layout
+
+SETTINGS_WEIGHTS = {  # mpc_planner_jackalsimulator/config/settings.yaml:78-92
+    "acceleration": 0.34, "angular_velocity": 0.85, "velocity": 0.55,
+    "reference_velocity": 2.0, "contour": 0.05, "lag": 0.75,
+    "terminal_angle": 100.0, "terminal_contouring": 10.0, "consistency": 0.05,
+}
+ROBOT_RADIUS = 0.325          # settings.yaml:38
+OBSTACLE_RADIUS = 0.325       # settings.yaml:43
+DECELERATION = 3.0            # settings.yaml:36 deceleration_at_infeasible
+SEED0 = 20251212
+
+
+@dataclass
+class Batch:
+    """Inputs of B*G independent solves, solve index = scene*G + guess."""
+    params: np.ndarray   # (B*G, N, npar)   horizon-major all_parameters
+    warm: np.ndarray     # (B*G, N+1, 7)    [u x] per stage (AcadosParameters::x0)
+    xinit: np.ndarray    # (B*G, 5)
+    guided: np.ndarray   # (B*G,) bool, False for the non-guided (T-MPC++) planner
+    n_scenes: int
+    n_guesses: int
+    prev_traj: np.ndarray  # (B, N, 2) interpolated previous trajectory (consistency reference)
+
+
+def _path(rng, n_seg):
+    """Cubic Hermite segments through a random smooth curve: segment length
+    U[3,6] m, heading change U[-0.6, 0.6] rad per segment."""
+    coef = np.zeros((n_seg, 2, 4))
+    starts = np.zeros(n_seg)
+    px, py = rng.uniform(-5, 5), rng.uniform(-5, 5)
+    th = rng.uniform(-np.pi, np.pi)
+    s0 = 0.0
+    for j in range(n_seg):
+        L = rng.uniform(3.0, 6.0)
+        th1 = th + rng.uniform(-0.6, 0.6)
+        c0 = np.array([np.cos(th), np.sin(th)])
+        c1 = np.array([np.cos(th1), np.sin(th1)])
+        p0 = np.array([px, py])
+        p1 = p0 + L * 0.5 * (c0 + c1)
+        A = np.array([[L ** 3, L ** 2], [3 * L ** 2, 2 * L]])
+        for ax in range(2):
+            a_, b_ = np.linalg.solve(A, [p1[ax] - p0[ax] - c0[ax] * L, c1[ax] - c0[ax]])
+            coef[j, ax] = (a_, b_, c0[ax], p0[ax])
+        starts[j] = s0
+        s0 += L
+        px, py, th = p1[0], p1[1], th1
+    return coef, starts
+
+
+def _path_eval(coef, starts, s):
+    """Plain (un-glued) piecewise evaluation used only to place scene objects."""
+    j = int(np.clip(np.searchsorted(starts, s, side="right") - 1, 0, len(starts) - 1))
+    t = s - starts[j]
+    a, b, c, d = coef[j, :, 0], coef[j, :, 1], coef[j, :, 2], coef[j, :, 3]
+    pos = a * t ** 3 + b * t ** 2 + c * t + d
+    der = 3 * a * t ** 2 + 2 * b * t + c
+    return pos, der / np.linalg.norm(der)
+
+
+def _braking(x0, N, dt):
+    """Solver::initializeWithBraking (acados_solver_interface.cpp:528-567)."""
+    warm = np.zeros((N + 1, 7))
+    x, y, psi, v, s = x0
+    a = -abs(DECELERATION)
+    warm[0] = (a, 0.0, x, y, psi, v, s)
+    for k in range(1, N + 1):
+        x += v * dt * np.cos(psi)
+        y += v * dt * np.sin(psi)
+        s += v * dt
+        v = max(v + a * dt, 0.0)
+        warm[k] = (a, 0.0, x, y, psi, v, s)
+    return warm
+
+
+def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
+    """A collision-free guidance trajectory (stand-in for the external
+    guidance_planner's PRM output): nominal progress along the path at v_ref,
+    a lateral offset that passes obstacle j on side signs[j] (+1 left, -1
+    right) with clearance, then a radial push-out so that every sample keeps
+    `CLEAR` metres from every predicted obstacle position (the space-time
+    search of guidance_planner only returns collision-free paths).
+    Returns positions and velocities at t = k*dt, k = 0..N."""
+    coef, starts, s_ego = tangent_path
+    CLEAR = 0.8
+    fine = np.linspace(0, N * dt, 8 * N + 1)
+    # progress: start at the ego speed, accelerate at 1 m/s^2 towards v_ref
+    v0 = ego[3]
+    vt = np.minimum(v0 + 1.0 * fine, max(vref, v0))
+    s_nom = s_ego + np.concatenate([[0.0], np.cumsum(0.5 * (vt[1:] + vt[:-1]) * np.diff(fine))])
+    ev = [_path_eval(coef, starts, s) for s in s_nom]
+    nom = np.array([e[0] for e in ev])
+    tan = np.array([e[1] for e in ev])
+    nrm = np.stack([-tan[:, 1], tan[:, 0]], 1)
+    off = np.zeros(len(fine))
+    for j, (op, ov) in enumerate(obstacles):
+        ob = op[None, :] + ov[None, :] * fine[:, None]
+        d = np.linalg.norm(nom - ob, axis=1)
+        ic = int(np.argmin(d))
+        lat = float(np.sum((ob[ic] - nom[ic]) * nrm[ic]))
+        want = lat + signs[j] * (CLEAR + 0.4)
+        if signs[j] * want < 0:  # already on the requested side with margin
+            continue
+        off += want * np.exp(-0.5 * ((fine - fine[ic]) / 1.2) ** 2) * (1.0 - np.exp(-fine / 0.8))
+    desired = nom + off[:, None] * nrm
+    desired = desired - desired[0] + ego[:2]
+    # track the desired path with a pure-pursuit unicycle inside the input
+    # bounds (|a| <= 2, |w| <= 0.8), so the guess is kinematically reachable
+    # from the current state, as guidance_planner's start-state-aware search is
+    h = fine[1] - fine[0]
+    x, y, psi, v = ego[0], ego[1], ego[2], ego[3]
+    traj = np.zeros_like(desired)
+    for i, t in enumerate(fine):
+        traj[i] = (x, y)
+        look = max(0.6, 0.6 * v)
+        j = min(len(fine) - 1, int(np.searchsorted(fine, t + look / max(vt[i], 0.3))))
+        tx, ty = desired[j] - (x, y)
+        alpha = np.arctan2(ty, tx) - psi
+        alpha = (alpha + np.pi) % (2 * np.pi) - np.pi
+        w = np.clip(2.0 * max(v, 0.3) * np.sin(alpha) / max(np.hypot(tx, ty), 0.3), -0.8, 0.8)
+        a = np.clip(2.0 * (vt[i] - v), -2.0, 2.0)
+        x += h * v * np.cos(psi)
+        y += h * v * np.sin(psi)
+        psi += h * w
+        v = max(v + h * a, 0.0)
+    vel = np.gradient(traj, fine, axis=0)
+    idx = np.searchsorted(fine, np.arange(N + 1) * dt - 1e-12)
+    return traj[idx], vel[idx]
+
+
+def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
+               seed: int = SEED0, first_scene: int = 0, consistency: bool = True) -> Batch:
+    N, npar, dt = layout.N, layout.npar, layout.dt
+    n_obs = layout.max_obstacles if n_obs is None else n_obs
+    assert n_obs <= layout.max_obstacles
+    G = n_guesses
+    S = n_scenes * G
+    params = np.zeros((S, N, npar))
+    warm = np.zeros((S, N + 1, 7))
+    xinit = np.zeros((S, 5))
+    guided = np.zeros(S, bool)
+    prev = np.zeros((n_scenes, N, 2))
+    ix = layout.idx
+    for sc in range(n_scenes):
+        rng = np.random.default_rng(seed + first_scene + sc)
+        coef, starts = _path(rng, layout.n_seg)
+        s_ego = rng.uniform(0.0, 1.0)
+        p_on, t_on = _path_eval(coef, starts, s_ego)
+        n_on = np.array([-t_on[1], t_on[0]])
+        ego_pos = p_on + rng.normal(0, 0.2) * n_on
+        v0 = rng.uniform(0.0, 2.0)
+        psi0 = np.arctan2(t_on[1], t_on[0]) + rng.normal(0.0, 0.1)
+        x0 = np.array([ego_pos[0], ego_pos[1], psi0, v0, s_ego])
+        obstacles = []
+        for j in range(n_obs):
+            ahead = rng.uniform(2.0, 10.0)
+            lat = rng.uniform(-3.0, 3.0)
+            pj, tj = _path_eval(coef, starts, s_ego + ahead)
+            nj = np.array([-tj[1], tj[0]])
+            obstacles.append((pj + lat * nj, rng.normal(0.0, 0.7, size=2)))
+        # scene-shared parameters (identical for every planner and stage)
+        base = np.zeros(npar)
+        for name, key in (("acceleration", "acceleration"), ("angular_velocity", "angular_velocity"),
+                          ("velocity", "velocity"), ("reference_velocity", "reference_velocity"),
+                          ("contour", "contour"), ("lag", "lag"), ("terminal_angle", "terminal_angle"),
+                          ("terminal_contouring", "terminal_contouring")):
+            base[ix(name)] = SETTINGS_WEIGHTS[key]
+        for j in range(layout.n_seg):
+            for ax, axn in enumerate("xy"):
+                for ci, cn in enumerate("abcd"):
+                    base[ix(f"spline_{axn}{j}_{cn}")] = coef[j, ax, ci]
+            base[ix(f"spline{j}_start")] = starts[j]
+        base[ix("ego_disc_radius")] = ROBOT_RADIUS
+        base[ix("ego_disc_0_offset")] = 0.0
+        stage = np.repeat(base[None, :], N, 0)
+        # ellipsoids: stage 0 dummies, stage k>=1 prediction k-1 (deterministic)
+        for j in range(layout.n_ell):
+            b0 = ix(f"ellipsoid_obst_{j}_x")
+            stage[0, b0:b0 + 7] = (x0[0] + 50.0, x0[1] + 50.0, 0.0, 0.0, 0.0, 1.0, 0.1)
+            if j < n_obs:
+                op, ov = obstacles[j]
+                for k in range(1, N):
+                    pk = op + ov * dt * (k - 1)
+                    stage[k, b0:b0 + 7] = (pk[0], pk[1], 0.0, 0.0, 0.0, 1.0, OBSTACLE_RADIUS)
+            else:  # ensureObstacleSize pads with far-away dummies (data_preparation.cpp:49-55)
+                for k in range(1, N):
+                    stage[k, b0:b0 + 7] = (x0[0] + 100.0, x0[1] + 100.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+        # consistency reference: the previous plan, i.e. a constant-speed
+        # roll-out along the initial heading (guidance_constraints.cpp:1073-1133)
+        vp = max(v0, 0.5)
+        for k in range(N):
+            prev[sc, k] = ego_pos + vp * dt * k * np.array([np.cos(psi0), np.sin(psi0)])
+        if layout.consistency:
+            wcons = SETTINGS_WEIGHTS["consistency"] if consistency else 0.0
+            for k in range(N):
+                valid = 1 <= k <= N - 2
+                stage[k, ix("consistency_weight")] = wcons if valid else 0.0
+                stage[k, ix("prev_traj_x")] = prev[sc, k, 0] if valid else 0.0
+                stage[k, ix("prev_traj_y")] = prev[sc, k, 1] if valid else 0.0
+        brake = _braking(x0.copy(), N, dt)
+        for g in range(G):
+            sidx = sc * G + g
+            P = stage.copy()
+            is_guided = g < G - 1
+            w = brake.copy()
+            lin = ix("lin_constraint_0_a1")
+            # dummies everywhere first (a1=1, a2=0, b=x+100: linearized_constraints.h:28, .cpp:54)
+            for i in range(layout.n_lin):
+                P[:, lin + 3 * i:lin + 3 * i + 3] = (1.0, 0.0, x0[0] + 100.0)
+            if is_guided:
+                signs = [1 if (g >> (j % 3)) & 1 else -1 for j in range(n_obs)]
+                if g >= 8:
+                    signs = list(np.random.default_rng(seed + 7919 * sidx).choice([-1, 1], n_obs))
+                pos, vel = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
+                                             SETTINGS_WEIGHTS["reference_velocity"])
+                for k in range(1, N):
+                    w[k, 2], w[k, 3] = pos[k]
+                    w[k, 4] = np.arctan2(vel[k, 1], vel[k, 0])
+                    w[k, 5] = np.linalg.norm(vel[k])
+                    for i in range(n_obs):
+                        op, ov = obstacles[i]
+                        ob = op + ov * dt * (k - 1)
+                        dxy = ob - pos[k]
+                        dist = np.linalg.norm(dxy)
+                        a1, a2 = dxy / dist
+                        bb = a1 * ob[0] + a2 * ob[1] - (1e-3 + ROBOT_RADIUS)
+                        P[k, lin + 3 * i:lin + 3 * i + 3] = (a1, a2, bb)
+            params[sidx] = P
+            warm[sidx] = w
+            xinit[sidx] = x0
+            guided[sidx] = is_guided
+    return Batch(params=params, warm=warm, xinit=xinit, guided=guided, n_scenes=n_scenes,
+                 n_guesses=G, prev_traj=prev)
