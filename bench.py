@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X T-MPC++ per-guess SQP backend.
+
+Workload (BASELINE.json configs[1], "C2"): jackal unicycle T-MPC++, N=20,
+8 obstacles, 1024 synthetic scenes x 8 topology guesses per GPU (7 guided +
+the non-guided T-MPC++ planner), 10 SQP-RTI iterations per solve, timeout
+disabled.  One step = one batched solve of all scenes x guesses + per-scene
+planner selection (FindBestPlanner) + one RCCL all-gather of the winning
+trajectories when N_gpus > 1 (scenes are sharded, weak scaling).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  `roofline` prices the solve kernel against HBM
+with SURVEY.md §8(d)'s algorithmic bytes per solve (the path is fp64-VALU /
+latency bound); `cpu_baseline` times the C oracle (same
+algorithm, OpenMP over solves) on a bounded sample of the same batch, and
+`parity` is max |x - x_ref| over that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "SQP solves/s (N=20, 8 obs, 8 guesses) at 1/2/4/8 MI355X; max |x−x_ref|"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (vendor spec)
+
+
+def algorithmic_bytes_per_solve(lay):
+    """B = 8*[N*npar + (N+1)*nvar + nx + (N+1)*nx + N*nu + 2]"""
+    N = lay.N
+    return 8 * (N * lay.npar + (N + 1) * lay.nvar + lay.nx + (N + 1) * lay.nx + N * lay.nu + 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--scenes", type=int, default=1024, help="scenes per GPU")
+    ap.add_argument("--guesses", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+    lay = config_layout(args.config)
+    S, G, N = args.scenes, args.guesses, lay.N
+    B = S * G
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    b = make_batch(lay, S, G, first_scene=rank * S, workers=min(threads, 16))
+    gen_s = time.time() - t0
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    params, warm, xinit = t(b.params), t(b.warm), t(b.xinit)
+    prev = t(b.prev_traj)
+    cons_en = torch.ones(B, dtype=torch.uint8, device=dev)
+    pr = native.problem_from_layout(lay)
+    out = dict(xtraj=torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev),
+               utraj=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+               pobj=torch.empty((B,), dtype=torch.float64, device=dev),
+               exit=torch.empty((B,), dtype=torch.int32, device=dev),
+               info=torch.empty((B, 4), dtype=torch.int32, device=dev))
+    win_w = (N + 1) * 5 + N * 2 + 2
+    winners = torch.empty((S, win_w), dtype=torch.float64, device=dev)
+    gathered = torch.empty((S * world, win_w), dtype=torch.float64, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    sidx = torch.arange(S, device=dev)
+
+    def step(i=None):
+        if i is not None:
+            ev_s[i].record(stream)
+        native.solve_batch_device(pr, params, warm, xinit, out=out, stream=stream)
+        if i is not None:
+            ev_e[i].record(stream)
+        best, _ = native.select_best_device(S, G, N, out["xtraj"], out["pobj"], out["exit"], prev_traj=prev,
+                                            w_cons=0.05, consistency_enabled=cons_en, stream=stream)
+        # winner record: xtraj | utraj | pobj | index  (index -1: all planners failed -> planner 0)
+        bi = best.long().clamp(min=0)
+        flat = sidx * G + bi
+        winners[:, :(N + 1) * 5] = out["xtraj"][flat].reshape(S, -1)
+        winners[:, (N + 1) * 5:(N + 1) * 5 + 2 * N] = out["utraj"][flat].reshape(S, -1)
+        winners[:, -2] = out["pobj"][flat]
+        winners[:, -1] = best.double()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, winners)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))
+    if world > 1:
+        te = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(te[0]), float(te[1])
+
+    total = args.steps * B * world
+    value = total / elapsed
+    exit_h = out["exit"].cpu().numpy()
+    xt_h = out["xtraj"].cpu().numpy()
+    info_h = out["info"].cpu().numpy()
+
+    bps = algorithmic_bytes_per_solve(lay)
+    achieved = bps * B / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("batch") == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "sqp_kernel", "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps}
+
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded scenes, SURVEY.md §8d)",
+        "config": {"workload": f"{args.config}: jackal unicycle T-MPC++, N={N}, {lay.max_obstacles} obstacles, "
+                               f"{S} scenes x {G} guesses per GPU, 10 SQP-RTI iterations",
+                   "scenes_per_gpu": S, "guesses": G, "N": N, "obstacles": lay.max_obstacles,
+                   "parallelism": f"scene-sharded x{world}" + (" + RCCL all-gather of winners" if world > 1 else "")},
+        "roofline": roofline,
+        "solver_stats": {"success_frac": float((exit_h == 1).mean()), "qp_iters_per_solve": float(info_h[:, 1].mean()),
+                         "scene_gen_s": round(gen_s, 2)},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        oracle_py.build()
+        orc = oracle_py.Oracle(lay)
+        # bounded sample: chunks of the same batch until ~cpu_seconds of CPU work
+        done, t_cpu, chunk = 0, 0.0, 256
+        max_abs_dx, agree, compared = 0.0, 0, 0
+        while done < B and t_cpu < args.cpu_seconds:
+            sl = slice(done, min(B, done + chunk))
+            tc = time.perf_counter()
+            ref = orc.solve_batch(b.params[sl], b.warm[sl], b.xinit[sl], nthreads=threads)
+            t_cpu += time.perf_counter() - tc
+            ok = (ref["status"] == 1) & (exit_h[sl] == 1)
+            if ok.any():
+                max_abs_dx = max(max_abs_dx, float(np.abs(xt_h[sl][ok] - ref["xtraj"][ok]).max()))
+            agree += int((ref["status"] == exit_h[sl]).sum())
+            compared += len(ref["status"])
+            done = sl.stop
+        tc = time.perf_counter()
+        n1 = 64
+        orc.solve_batch(b.params[:n1], b.warm[:n1], b.xinit[:n1], nthreads=1)
+        t1 = time.perf_counter() - tc
+        result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
+                                  "kind": "port",
+                                  "sample": f"first {done} of the {B} solves of this batch, C oracle "
+                                            f"(same algorithm), OpenMP {threads} threads",
+                                  "single_thread_solves_per_s": round(n1 / t1, 2)}
+        result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
+                            "solves_compared": compared, "tolerance": 1e-4}
+        result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+/*
+ * mpcg.h — C ABI of the MI355X-native T-MPC++ per-guess SQP backend.
+ *
+ * This is the drop-in boundary for the hot path of
+ * Juleszwanen/oscar_mpc_planner_mr_modification: the OpenMP fan-out of
+ * independent `MPCPlanner::Solver::solve()` calls inside
+ * `GuidanceConstraints::optimize` (mpc_planner_modules/src/guidance_constraints.cpp:304-421)
+ * and the acados SQP-RTI solve each of them runs
+ * (mpc_planner_solver/src/acados_solver_interface.cpp:311-429).
+ *
+ * Plain pointers and sizes only.  Buffers use the reference's own layouts:
+ *   params  [batch][N][npar]      == AcadosParameters::all_parameters, horizon-major
+ *                                    (mpc_planner_solver/include/mpc_planner_solver/acados_solver_interface.h:56)
+ *   warm    [batch][N+1][nu+nx]   == AcadosParameters::x0 = [u0 x0 | u1 x1 | ...] (:54)
+ *   xinit   [batch][nx]           == AcadosParameters::xinit (:53)
+ *   xtraj   [batch][N+1][nx]      == AcadosOutput::xtraj (:129)
+ *   utraj   [batch][N][nu]        == AcadosOutput::utraj (:130)
+ *   pobj    [batch]               == AcadosInfo::pobj (:108)
+ *   exit    [batch]               == return value of Solver::solve(): 1 success, 0 failure,
+ *                                    2 max-iter, 3 min-step, 4 QP failure (:423-428)
+ * Batch element b = scene * n_guesses + guess.
+ */
+#ifndef MPCG_H
+#define MPCG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCG_NX 5
+#define MPCG_NU 2
+#define MPCG_NVAR 7
+#define MPCG_ABI_VERSION 1
+
+/* Problem description: the generated solver's dimensions + the parameter
+ * map (parameter_map.yaml written by solver_generator/generate_solver.py:34-46)
+ * reduced to the base index of every parameter bundle the stage functions
+ * read, and the acados options of generate_acados_solver.py:88-173.
+ * -1 marks an absent module. */
+typedef struct mpcg_problem {
+    int N, npar;
+    int n_lin, n_ell, n_seg;
+    int i_w_acc, i_w_ang, i_w_vel, i_v_ref, i_w_contour, i_w_lag;
+    int i_spline0;                 /* segment j at i_spline0 + 9 j: xa xb xc xd ya yb yc yd start */
+    int i_cons_w, i_prev_x, i_prev_y;
+    int i_lin0;                    /* halfspace i at i_lin0 + 3 i: a1 a2 b */
+    int i_disc_r, i_disc_off;
+    int i_ell0;                    /* obstacle j at i_ell0 + 7 j: x y psi major minor chi r */
+    double dt;                     /* integrator_step; ERK4 over dt with rk_steps steps */
+    int rk_steps;
+    double lbu[MPCG_NU], ubu[MPCG_NU], lbx[MPCG_NX], ubx[MPCG_NX];
+    int sqp_iters;                 /* solver_settings.acados.iterations (timeout disabled) */
+    double qp_tol;                 /* 1e-5 */
+    int qp_iter_max;               /* 50 */
+    double reg_eps;                /* MIRROR epsilon 1e-4 */
+    double qp_mu0, qp_thr0;        /* interior-point cold start */
+    double res_eq_fail;            /* 1e-2 */
+} mpcg_problem;
+
+/* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,
+ * last QP status (0 ok, 1 nan/diverged, 2 max-iter, 3 min-step), reserved */
+#define MPCG_INFO_STRIDE 4
+
+int mpcg_abi_version(void);
+const char *mpcg_last_error(void);
+
+/* 0 if (N, n_lin, n_ell) has a compiled kernel instance, else -1 */
+int mpcg_supported(const mpcg_problem *pr);
+
+/* Batched solve, every pointer in device memory, enqueued on `stream`
+ * (a hipStream_t, NULL = default stream).  Returns 0 on successful launch. */
+int mpcg_solve_batch_device(const mpcg_problem *pr, int batch,
+                            const double *params, const double *warm, const double *xinit,
+                            double *xtraj, double *utraj, double *pobj, int *exit_code,
+                            int *info, void *stream);
+
+/* Same with host buffers: copies in, solves, copies out, synchronises.
+ * This is what one `Solver::solve()` call maps to (batch = 1). */
+int mpcg_solve_batch_host(const mpcg_problem *pr, int batch,
+                          const double *params, const double *warm, const double *xinit,
+                          double *xtraj, double *utraj, double *pobj, int *exit_code, int *info);
+
+/* Planner selection per scene == the objective bookkeeping of
+ * GuidanceConstraints::optimize (guidance_constraints.cpp:372-420) followed
+ * by FindBestPlanner (:572-590):
+ *   obj_g = pobj_g - [consistency_g] * w_cons * sum_{k=1}^{N-2} |xy_k - prev_k|^2
+ *   obj_g *= selection_weight            if previously_selected_g
+ *   best  = argmin obj_g over !disabled && exit == 1, -1 if none (first index wins ties)
+ * prev_traj: [n_scenes][N][2] or NULL; flags: [n_scenes][G] bytes, may be NULL.
+ * best: [n_scenes], objective out: [n_scenes][G] (may be NULL).  Device pointers. */
+int mpcg_select_best_device(int n_scenes, int n_guesses, int N,
+                            const double *xtraj, const double *pobj, const int *exit_code,
+                            const double *prev_traj, double w_cons,
+                            const unsigned char *consistency_enabled,
+                            const unsigned char *previously_selected, double selection_weight,
+                            const unsigned char *disabled,
+                            int *best, double *objective, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCG_H */

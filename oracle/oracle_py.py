@@ -96,7 +96,7 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.qp_iter_max = opts.get("qp_iter_max", 50)
     pr.reg_eps = opts.get("reg_eps", 1e-4)
     pr.qp_mu0 = opts.get("qp_mu0", 1.0)
-    pr.qp_thr0 = opts.get("qp_thr0", 1e-2)
+    pr.qp_thr0 = opts.get("qp_thr0", 1.0)
     pr.res_eq_fail = opts.get("res_eq_fail", 1e-2)
     return pr
 

@@ -1,0 +1,317 @@
+// mpcg_device.h — per-stage device functions of the T-MPC++ SQP backend
+// (gfx950, fp64 VALU).  One lane evaluates one shooting stage.
+//
+// Reference semantics (paths relative to the reference repo):
+//   stage cost   solver_definition.py:19-34 over mpc_base.py:47-60,
+//                contouring.py:140-174 (stage_idx=1), consistency_module.py:229-250,
+//                glued spline spline.py:28-86
+//   constraints  guidance_constraints.py:355-370 then ellipsoid_constraints.py:435-489
+//   dynamics     solver_model.py:207-214 integrated by acados ERK (4 stages,
+//                3 steps) with exact first/second-order sensitivities
+//                (generate_acados_solver.py:148-157)
+//   MIRROR       regularize_method "MIRROR" (generate_acados_solver.py:157)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcg.h"
+
+namespace mpcg {
+
+constexpr int NX = MPCG_NX, NU = MPCG_NU, NZ = MPCG_NVAR;
+
+// ---------------------------------------------------------------------------
+// glued spline of spline.py:39-58: for both axes the glued position G and the
+// glued segment-derivative D, each with first and second s-derivatives.
+// ---------------------------------------------------------------------------
+struct SplineJets {
+    double Gx[3], Gy[3], Dx[3], Dy[3];
+};
+
+__device__ __forceinline__ void seg_jets(const double* __restrict__ c, double t, double P[4]) {
+    // c = (a, b, c, d); P = (P, P', P'', P''')
+    double a = c[0], b = c[1], cc = c[2], d = c[3];
+    P[0] = ((a * t + b) * t + cc) * t + d;
+    P[1] = (3.0 * a * t + 2.0 * b) * t + cc;
+    P[2] = 6.0 * a * t + 2.0 * b;
+    P[3] = 6.0 * a;
+}
+
+__device__ inline void spline_jets(const mpcg_problem& pr, const double* __restrict__ p, double s,
+                                   SplineJets& J) {
+    const int M = pr.n_seg;
+    const double* base = p + pr.i_spline0;
+    double Px[4], Py[4];
+    {
+        const double* seg = base + 9 * (M - 1);
+        double t = s - seg[8];
+        seg_jets(seg, t, Px);
+        seg_jets(seg + 4, t, Py);
+    }
+    double Vx[3] = {Px[0], Px[1], Px[2]}, Wx[3] = {Px[1], Px[2], Px[3]};
+    double Vy[3] = {Py[0], Py[1], Py[2]}, Wy[3] = {Py[1], Py[2], Py[3]};
+    for (int k = M - 1; k >= 1; --k) {
+        // lambda_k uses the start of segment k (spline.py:37)
+        const double sk = base[9 * k + 8];
+        const double e = exp((s - sk + 0.02) / 0.1);
+        const double l0 = 1.0 / (1.0 + e);
+        const double l1 = -10.0 * l0 * (1.0 - l0);
+        const double l2 = 100.0 * l0 * (1.0 - l0) * (1.0 - 2.0 * l0);
+        const double* seg = base + 9 * (k - 1);
+        const double t = s - seg[8];
+        seg_jets(seg, t, Px);
+        seg_jets(seg + 4, t, Py);
+        const double m0 = 1.0 - l0;
+        // glued value and its derivatives
+        double a0 = Px[0] - Vx[0], a1 = Px[1] - Vx[1];
+        Vx[2] = l2 * a0 + 2.0 * l1 * a1 + l0 * Px[2] + m0 * Vx[2];
+        Vx[1] = l1 * a0 + l0 * Px[1] + m0 * Vx[1];
+        Vx[0] = l0 * Px[0] + m0 * Vx[0];
+        a0 = Py[0] - Vy[0]; a1 = Py[1] - Vy[1];
+        Vy[2] = l2 * a0 + 2.0 * l1 * a1 + l0 * Py[2] + m0 * Vy[2];
+        Vy[1] = l1 * a0 + l0 * Py[1] + m0 * Vy[1];
+        Vy[0] = l0 * Py[0] + m0 * Vy[0];
+        // glued segment derivative and its derivatives
+        a0 = Px[1] - Wx[0]; a1 = Px[2] - Wx[1];
+        Wx[2] = l2 * a0 + 2.0 * l1 * a1 + l0 * Px[3] + m0 * Wx[2];
+        Wx[1] = l1 * a0 + l0 * Px[2] + m0 * Wx[1];
+        Wx[0] = l0 * Px[1] + m0 * Wx[0];
+        a0 = Py[1] - Wy[0]; a1 = Py[2] - Wy[1];
+        Wy[2] = l2 * a0 + 2.0 * l1 * a1 + l0 * Py[3] + m0 * Wy[2];
+        Wy[1] = l1 * a0 + l0 * Py[2] + m0 * Wy[1];
+        Wy[0] = l0 * Py[1] + m0 * Wy[0];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        J.Gx[i] = Vx[i]; J.Gy[i] = Vy[i]; J.Dx[i] = Wx[i]; J.Dy[i] = Wy[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stage cost L(z; p), gradient and Hessian (z = [a, w, x, y, psi, v, s])
+// ---------------------------------------------------------------------------
+__device__ inline double stage_cost(const mpcg_problem& pr, const double* __restrict__ p,
+                                    const double z[NZ], double g[NZ], double H[NZ][NZ], bool derivs) {
+    const double a = z[0], w = z[1], x = z[2], y = z[3], v = z[5], s = z[6];
+    const double wa = p[pr.i_w_acc], ww = p[pr.i_w_ang], wv = p[pr.i_w_vel], vref = p[pr.i_v_ref];
+    const double wc = p[pr.i_w_contour], wl = p[pr.i_w_lag];
+    double L = wa * a * a + ww * w * w + wv * (v - vref) * (v - vref);
+    SplineJets J;
+    spline_jets(pr, p, s, J);
+    const double r = sqrt(J.Dx[0] * J.Dx[0] + J.Dy[0] * J.Dy[0]);
+    const double ir = 1.0 / r;
+    const double tx = J.Dx[0] * ir, ty = J.Dy[0] * ir;
+    const double ex = x - J.Gx[0], ey = y - J.Gy[0];
+    const double ec = ty * ex - tx * ey;  // contour error (contouring.py:166)
+    const double el = tx * ex + ty * ey;  // lag error (contouring.py:167)
+    L += wl * el * el + wc * ec * ec;
+    double wcn = 0.0, dxp = 0.0, dyp = 0.0;
+    if (pr.i_cons_w >= 0) {
+        wcn = p[pr.i_cons_w];
+        dxp = x - p[pr.i_prev_x];
+        dyp = y - p[pr.i_prev_y];
+        L += wcn * (dxp * dxp + dyp * dyp);
+    }
+    if (!derivs) return L;
+    const double r1 = tx * J.Dx[1] + ty * J.Dy[1];
+    const double tx1 = (J.Dx[1] - tx * r1) * ir, ty1 = (J.Dy[1] - ty * r1) * ir;
+    const double r2 = tx1 * J.Dx[1] + ty1 * J.Dy[1] + tx * J.Dx[2] + ty * J.Dy[2];
+    const double tx2 = (J.Dx[2] - 2.0 * tx1 * r1 - tx * r2) * ir;
+    const double ty2 = (J.Dy[2] - 2.0 * ty1 * r1 - ty * r2) * ir;
+    const double Gx1 = J.Gx[1], Gy1 = J.Gy[1], Gx2 = J.Gx[2], Gy2 = J.Gy[2];
+    // d(e)/d(x, y, s) and the s-row of the second derivatives
+    const double dc[3] = {ty, -tx, ty1 * ex - tx1 * ey - ty * Gx1 + tx * Gy1};
+    const double dl[3] = {tx, ty, tx1 * ex + ty1 * ey - tx * Gx1 - ty * Gy1};
+    const double hc_s[3] = {ty1, -tx1, ty2 * ex - tx2 * ey - 2.0 * ty1 * Gx1 + 2.0 * tx1 * Gy1 - ty * Gx2 + tx * Gy2};
+    const double hl_s[3] = {tx1, ty1, tx2 * ex + ty2 * ey - 2.0 * tx1 * Gx1 - 2.0 * ty1 * Gy1 - tx * Gx2 - ty * Gy2};
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+        g[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) H[i][j] = 0.0;
+    }
+    g[0] = 2.0 * wa * a; H[0][0] = 2.0 * wa;
+    g[1] = 2.0 * ww * w; H[1][1] = 2.0 * ww;
+    g[5] = 2.0 * wv * (v - vref); H[5][5] = 2.0 * wv;
+    constexpr int ids[3] = {2, 3, 6};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        g[ids[i]] += 2.0 * (wl * el * dl[i] + wc * ec * dc[i]);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            // second derivatives of e vanish on the (x,y)x(x,y) block
+            double hl = (i == 2) ? hl_s[j] : ((j == 2) ? hl_s[i] : 0.0);
+            double hc = (i == 2) ? hc_s[j] : ((j == 2) ? hc_s[i] : 0.0);
+            H[ids[i]][ids[j]] += 2.0 * (wl * (dl[i] * dl[j] + el * hl) + wc * (dc[i] * dc[j] + ec * hc));
+        }
+    }
+    if (pr.i_cons_w >= 0) {
+        g[2] += 2.0 * wcn * dxp; g[3] += 2.0 * wcn * dyp;
+        H[2][2] += 2.0 * wcn; H[3][3] += 2.0 * wcn;
+    }
+    return L;
+}
+
+// ---------------------------------------------------------------------------
+// acados ERK4 (rk_steps steps over dt) of the contouring unicycle
+// x' = (v cos psi, v sin psi, w, a, v).  psi and v are affine in time inside
+// a shooting interval (psi_e = psi + tau_e w, v_e = v + tau_e a at every RK
+// stage argument), so the discrete map is exactly
+//   x+ = x + sum_e h b_e v_e cos(psi_e), y+ likewise with sin, s+ = s + sum_e h b_e v_e,
+//   psi+ = psi + dt w, v+ = v + dt a,
+// and its exact Jacobian / second-order adjoint follow in closed form.
+// Outputs F = [B A] (5x7), xn, and (if pi != nullptr) H += Hess(pi' x+).
+// ---------------------------------------------------------------------------
+__device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NZ], const double* pi,
+                                    double xn[NX], double F[NX][NZ], double H[NZ][NZ]) {
+    const double a = z[0], w = z[1], psi = z[4], v = z[5];
+    const int ns = pr.rk_steps;
+    const double h = pr.dt / ns;
+    // c_q = (0, 1/2, 1/2, 1), b_q = (1, 2, 2, 1)/6
+    double sx = 0.0, sy = 0.0, ss = 0.0;
+    // d/d(a, w, psi, v) of sum b v_e cos, sum b v_e sin, sum b v_e
+    double jx[4] = {0, 0, 0, 0}, jy[4] = {0, 0, 0, 0}, js[4] = {0, 0, 0, 0};
+    // Hessian accumulators over (a, w, psi, v)
+    double hq[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hq[i][j] = 0.0;
+    const double pix = pi ? pi[0] : 0.0, piy = pi ? pi[1] : 0.0;
+    double cpsi, spsi;
+    sincos(psi, &spsi, &cpsi);
+    for (int st = 0; st < ns; ++st) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double cq = (q == 0) ? 0.0 : ((q == 3) ? 1.0 : 0.5);
+            const double bq = ((q == 0 || q == 3) ? 1.0 : 2.0) * h / 6.0;
+            const double tau = (st + cq) * h;
+            double sw, cw;
+            sincos(tau * w, &sw, &cw);
+            const double ce = cpsi * cw - spsi * sw;  // cos(psi + tau w)
+            const double se = spsi * cw + cpsi * sw;  // sin(psi + tau w)
+            const double ve = v + tau * a;
+            sx += bq * ve * ce;
+            sy += bq * ve * se;
+            ss += bq * ve;
+            // d psi_e = (0, tau, 1, 0), d v_e = (tau, 0, 0, 1) over (a, w, psi, v)
+            const double dcx_p = -ve * se, dcx_v = ce;   // d(v cos)/d(psi_e, v_e)
+            const double dcy_p = ve * ce, dcy_v = se;    // d(v sin)/d(psi_e, v_e)
+            jx[0] += bq * dcx_v * tau; jx[1] += bq * dcx_p * tau; jx[2] += bq * dcx_p; jx[3] += bq * dcx_v;
+            jy[0] += bq * dcy_v * tau; jy[1] += bq * dcy_p * tau; jy[2] += bq * dcy_p; jy[3] += bq * dcy_v;
+            js[0] += bq * tau; js[3] += bq;
+            if (pi) {
+                // second derivatives of pix v cos + piy v sin in (psi_e, v_e)
+                const double hpp = bq * (-pix * ve * ce - piy * ve * se);
+                const double hpv = bq * (-pix * se + piy * ce);
+                const double rp[4] = {0.0, tau, 1.0, 0.0};
+                const double rv[4] = {tau, 0.0, 0.0, 1.0};
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        hq[i][j] += hpp * rp[i] * rp[j] + hpv * (rp[i] * rv[j] + rv[i] * rp[j]);
+            }
+        }
+    }
+    const double T = pr.dt;
+    xn[0] = z[2] + sx;
+    xn[1] = z[3] + sy;
+    xn[2] = psi + T * w;
+    xn[3] = v + T * a;
+    xn[4] = z[6] + ss;
+    // F = d x+ / d z, z = [a, w, x, y, psi, v, s]
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) F[i][j] = 0.0;
+    constexpr int zi[4] = {0, 1, 4, 5};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        F[0][zi[j]] = jx[j];
+        F[1][zi[j]] = jy[j];
+        F[4][zi[j]] = js[j];
+    }
+    F[0][2] = 1.0; F[1][3] = 1.0; F[4][6] = 1.0;
+    F[2][1] = T; F[2][4] = 1.0;
+    F[3][0] = T; F[3][5] = 1.0;
+    if (pi) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) H[zi[i]][zi[j]] += hq[i][j];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MIRROR: H <- V f(D) V', f(d) = eps if |d| <= eps else |d|, cyclic Jacobi
+// on the 7x7 stage block.  Rotations on exactly-zero couplings are skipped,
+// so decoupled sub-blocks (e.g. {a,w,psi,v} vs {x,y,s} with a zero disc
+// offset) cost only their own rotations.
+// ---------------------------------------------------------------------------
+__device__ inline void mirror7(double A[NZ][NZ], double eps) {
+    double V[NZ][NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i)
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) {
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+            if (j > i) { double m = 0.5 * (A[i][j] + A[j][i]); A[i][j] = m; A[j][i] = m; }
+        }
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0.0, dia = 0.0;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) {
+            dia += A[i][i] * A[i][i];
+#pragma unroll
+            for (int j = i + 1; j < NZ; ++j) off += A[i][j] * A[i][j];
+        }
+        if (off <= 1e-32 * dia || off < 1e-300) break;
+#pragma unroll
+        for (int p = 0; p < NZ - 1; ++p)
+#pragma unroll
+            for (int q = p + 1; q < NZ; ++q) {
+                const double apq = A[p][q];
+                if (fabs(apq) >= 1e-300) {
+                    const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+                    const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+                    for (int k = 0; k < NZ; ++k) {
+                        const double akp = A[k][p], akq = A[k][q];
+                        A[k][p] = c * akp - s * akq;
+                        A[k][q] = s * akp + c * akq;
+                    }
+#pragma unroll
+                    for (int k = 0; k < NZ; ++k) {
+                        const double apk = A[p][k], aqk = A[q][k];
+                        A[p][k] = c * apk - s * aqk;
+                        A[q][k] = s * apk + c * aqk;
+                    }
+#pragma unroll
+                    for (int k = 0; k < NZ; ++k) {
+                        const double vkp = V[k][p], vkq = V[k][q];
+                        V[k][p] = c * vkp - s * vkq;
+                        V[k][q] = s * vkp + c * vkq;
+                    }
+                }
+            }
+    }
+    double d[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+        double di = A[i][i];
+        d[i] = (di >= -eps && di <= eps) ? eps : fabs(di);
+    }
+#pragma unroll
+    for (int i = 0; i < NZ; ++i)
+#pragma unroll
+        for (int j = i; j < NZ; ++j) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) acc += V[i][k] * d[k] * V[j][k];
+            A[i][j] = acc;
+            A[j][i] = acc;
+        }
+}
+
+}  // namespace mpcg

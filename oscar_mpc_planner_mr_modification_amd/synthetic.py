@@ -23,6 +23,7 @@ batch (e.g. one GPU's shard) regenerates bit-identically.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 
 import numpy as np
@@ -78,13 +79,15 @@ def _path(rng, n_seg):
 
 
 def _path_eval(coef, starts, s):
-    """Plain (un-glued) piecewise evaluation used only to place scene objects."""
-    j = int(np.clip(np.searchsorted(starts, s, side="right") - 1, 0, len(starts) - 1))
-    t = s - starts[j]
+    """Plain (un-glued) piecewise evaluation used only to place scene objects;
+    `s` scalar or array."""
+    s = np.asarray(s, dtype=float)
+    j = np.clip(np.searchsorted(starts, s, side="right") - 1, 0, len(starts) - 1)
+    t = (s - starts[j])[..., None]
     a, b, c, d = coef[j, :, 0], coef[j, :, 1], coef[j, :, 2], coef[j, :, 3]
-    pos = a * t ** 3 + b * t ** 2 + c * t + d
-    der = 3 * a * t ** 2 + 2 * b * t + c
-    return pos, der / np.linalg.norm(der)
+    pos = ((a * t + b) * t + c) * t + d
+    der = (3 * a * t + 2 * b) * t + c
+    return pos, der / np.linalg.norm(der, axis=-1, keepdims=True)
 
 
 def _braking(x0, N, dt):
@@ -117,9 +120,7 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
     v0 = ego[3]
     vt = np.minimum(v0 + 1.0 * fine, max(vref, v0))
     s_nom = s_ego + np.concatenate([[0.0], np.cumsum(0.5 * (vt[1:] + vt[:-1]) * np.diff(fine))])
-    ev = [_path_eval(coef, starts, s) for s in s_nom]
-    nom = np.array([e[0] for e in ev])
-    tan = np.array([e[1] for e in ev])
+    nom, tan = _path_eval(coef, starts, s_nom)
     nrm = np.stack([-tan[:, 1], tan[:, 0]], 1)
     off = np.zeros(len(fine))
     for j, (op, ov) in enumerate(obstacles):
@@ -136,20 +137,24 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
     # track the desired path with a pure-pursuit unicycle inside the input
     # bounds (|a| <= 2, |w| <= 0.8), so the guess is kinematically reachable
     # from the current state, as guidance_planner's start-state-aware search is
-    h = fine[1] - fine[0]
-    x, y, psi, v = ego[0], ego[1], ego[2], ego[3]
+    h = float(fine[1] - fine[0])
+    x, y, psi, v = float(ego[0]), float(ego[1]), float(ego[2]), float(ego[3])
     traj = np.zeros_like(desired)
-    for i, t in enumerate(fine):
-        traj[i] = (x, y)
+    des = desired.tolist()
+    vtl = vt.tolist()
+    nf = len(fine)
+    for i in range(nf):
+        traj[i, 0] = x
+        traj[i, 1] = y
         look = max(0.6, 0.6 * v)
-        j = min(len(fine) - 1, int(np.searchsorted(fine, t + look / max(vt[i], 0.3))))
-        tx, ty = desired[j] - (x, y)
-        alpha = np.arctan2(ty, tx) - psi
-        alpha = (alpha + np.pi) % (2 * np.pi) - np.pi
-        w = np.clip(2.0 * max(v, 0.3) * np.sin(alpha) / max(np.hypot(tx, ty), 0.3), -0.8, 0.8)
-        a = np.clip(2.0 * (vt[i] - v), -2.0, 2.0)
-        x += h * v * np.cos(psi)
-        y += h * v * np.sin(psi)
+        j = min(nf - 1, i + int(math.ceil(look / max(vtl[i], 0.3) / h - 1e-9)))
+        tx, ty = des[j][0] - x, des[j][1] - y
+        alpha = math.atan2(ty, tx) - psi
+        alpha = (alpha + math.pi) % (2 * math.pi) - math.pi
+        w = min(0.8, max(-0.8, 2.0 * max(v, 0.3) * math.sin(alpha) / max(math.hypot(tx, ty), 0.3)))
+        a = min(2.0, max(-2.0, 2.0 * (vtl[i] - v)))
+        x += h * v * math.cos(psi)
+        y += h * v * math.sin(psi)
         psi += h * w
         v = max(v + h * a, 0.0)
     vel = np.gradient(traj, fine, axis=0)
@@ -158,7 +163,26 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
 
 
 def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
-               seed: int = SEED0, first_scene: int = 0, consistency: bool = True) -> Batch:
+               seed: int = SEED0, first_scene: int = 0, consistency: bool = True, workers: int = 1) -> Batch:
+    """Scenes [first_scene, first_scene + n_scenes) x n_guesses planners.  With
+    workers > 1 the scenes are generated in a process pool; per-scene seeding
+    makes the result identical to the serial one."""
+    if workers > 1 and n_scenes >= 2 * workers:
+        from concurrent.futures import ProcessPoolExecutor
+
+        chunks = np.array_split(np.arange(n_scenes), workers)
+        with ProcessPoolExecutor(max_workers=workers) as ex:
+            futs = [ex.submit(_make_batch_serial, layout, len(c), n_guesses, n_obs, seed, first_scene + int(c[0]),
+                              consistency) for c in chunks if len(c)]
+            parts = [f.result() for f in futs]
+        return Batch(params=np.concatenate([p.params for p in parts]), warm=np.concatenate([p.warm for p in parts]),
+                     xinit=np.concatenate([p.xinit for p in parts]), guided=np.concatenate([p.guided for p in parts]),
+                     n_scenes=n_scenes, n_guesses=n_guesses, prev_traj=np.concatenate([p.prev_traj for p in parts]))
+    return _make_batch_serial(layout, n_scenes, n_guesses, n_obs, seed, first_scene, consistency)
+
+
+def _make_batch_serial(layout: Layout, n_scenes: int, n_guesses: int, n_obs: int | None,
+                       seed: int, first_scene: int, consistency: bool) -> Batch:
     N, npar, dt = layout.N, layout.npar, layout.dt
     n_obs = layout.max_obstacles if n_obs is None else n_obs
     assert n_obs <= layout.max_obstacles
@@ -208,12 +232,11 @@ def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | N
             stage[0, b0:b0 + 7] = (x0[0] + 50.0, x0[1] + 50.0, 0.0, 0.0, 0.0, 1.0, 0.1)
             if j < n_obs:
                 op, ov = obstacles[j]
-                for k in range(1, N):
-                    pk = op + ov * dt * (k - 1)
-                    stage[k, b0:b0 + 7] = (pk[0], pk[1], 0.0, 0.0, 0.0, 1.0, OBSTACLE_RADIUS)
+                kk = np.arange(N - 1)[:, None]
+                stage[1:, b0:b0 + 2] = op[None, :] + ov[None, :] * dt * kk
+                stage[1:, b0 + 2:b0 + 7] = (0.0, 0.0, 0.0, 1.0, OBSTACLE_RADIUS)
             else:  # ensureObstacleSize pads with far-away dummies (data_preparation.cpp:49-55)
-                for k in range(1, N):
-                    stage[k, b0:b0 + 7] = (x0[0] + 100.0, x0[1] + 100.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+                stage[1:, b0:b0 + 7] = (x0[0] + 100.0, x0[1] + 100.0, 0.0, 0.0, 0.0, 1.0, 0.0)
         # consistency reference: the previous plan, i.e. a constant-speed
         # roll-out along the initial heading (guidance_constraints.cpp:1073-1133)
         vp = max(v0, 0.5)
@@ -227,6 +250,10 @@ def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | N
                 stage[k, ix("prev_traj_x")] = prev[sc, k, 0] if valid else 0.0
                 stage[k, ix("prev_traj_y")] = prev[sc, k, 1] if valid else 0.0
         brake = _braking(x0.copy(), N, dt)
+        # obs_pred[k, i] = prediction k-1 of obstacle i (stage k >= 1)
+        obs_pred = np.zeros((N, n_obs, 2))
+        for i, (op, ov) in enumerate(obstacles):
+            obs_pred[1:, i] = op[None, :] + ov[None, :] * dt * np.arange(N - 1)[:, None]
         for g in range(G):
             sidx = sc * G + g
             P = stage.copy()
@@ -242,18 +269,20 @@ def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | N
                     signs = list(np.random.default_rng(seed + 7919 * sidx).choice([-1, 1], n_obs))
                 pos, vel = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
                                              SETTINGS_WEIGHTS["reference_velocity"])
-                for k in range(1, N):
-                    w[k, 2], w[k, 3] = pos[k]
-                    w[k, 4] = np.arctan2(vel[k, 1], vel[k, 0])
-                    w[k, 5] = np.linalg.norm(vel[k])
-                    for i in range(n_obs):
-                        op, ov = obstacles[i]
-                        ob = op + ov * dt * (k - 1)
-                        dxy = ob - pos[k]
-                        dist = np.linalg.norm(dxy)
-                        a1, a2 = dxy / dist
-                        bb = a1 * ob[0] + a2 * ob[1] - (1e-3 + ROBOT_RADIUS)
-                        P[k, lin + 3 * i:lin + 3 * i + 3] = (a1, a2, bb)
+                w[1:N, 2:4] = pos[1:N]
+                w[1:N, 4] = np.arctan2(vel[1:N, 1], vel[1:N, 0])
+                w[1:N, 5] = np.hypot(vel[1:N, 0], vel[1:N, 1])
+                if n_obs:
+                    # LinearizedConstraints::update (linearized_constraints.cpp:84-105)
+                    ob = obs_pred[1:N]                                # (N-1, n_obs, 2)
+                    dxy = ob - pos[1:N, None, :]
+                    dist = np.hypot(dxy[..., 0], dxy[..., 1])
+                    a1 = dxy[..., 0] / dist
+                    a2 = dxy[..., 1] / dist
+                    bb = a1 * ob[..., 0] + a2 * ob[..., 1] - (1e-3 + ROBOT_RADIUS)
+                    blk = P[1:N, lin:lin + 3 * n_obs].reshape(N - 1, n_obs, 3)
+                    blk[..., 0], blk[..., 1], blk[..., 2] = a1, a2, bb
+                    P[1:N, lin:lin + 3 * n_obs] = blk.reshape(N - 1, 3 * n_obs)
             params[sidx] = P
             warm[sidx] = w
             xinit[sidx] = x0
