@@ -68,6 +68,38 @@ struct Lds {
     int flag;
 };
 
+// Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
+// production build compiles them out).  Shares of a phase, not absolute times.
+#ifdef MPCG_STAMPS
+#define STAMP_DECL unsigned long long st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0_ = 0;
+#define STAMP_BEGIN()                                  \
+    do {                                               \
+        __syncthreads();                               \
+        st_t0_ = __builtin_amdgcn_s_memtime();         \
+    } while (0)
+#define STAMP_END(i)                                           \
+    do {                                                       \
+        __syncthreads();                                       \
+        st_acc_[i] += __builtin_amdgcn_s_memtime() - st_t0_;   \
+    } while (0)
+#define STAMP_STORE(ptr, sol)                                                      \
+    do {                                                                           \
+        if ((ptr) && threadIdx.x == 0)                                             \
+            for (int i_ = 0; i_ < 10; ++i_) (ptr)[(size_t)(sol) * 10 + i_] = st_acc_[i_]; \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END(i) do {} while (0)
+#define STAMP_STORE(ptr, sol) do {} while (0)
+#endif
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -202,8 +234,10 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
                                                  const double* __restrict__ xinit,
                                                  double* __restrict__ xtraj, double* __restrict__ utraj,
                                                  double* __restrict__ pobj_out, int* __restrict__ exit_out,
-                                                 int* __restrict__ info_out) {
+                                                 int* __restrict__ info_out,
+                                                 unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, NH = C::NH;
+    STAMP_DECL
     __shared__ Lds<C> S;
     const int sol = blockIdx.x;
     if (sol >= batch) return;
@@ -226,6 +260,7 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
 
     for (int it = 0; it < pr.sqp_iters; ++it) {
         // ================= preparation: linearise =================
+        STAMP_BEGIN();
         double resl = 0.0;
         if (lane < N) {
             linearize_stage<C>(pr, S, pbase + (size_t)lane * npar, lane, resl);
@@ -240,6 +275,8 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
         res_eq = wave_max(resl);
         if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
         __syncthreads();
+        STAMP_END(0);
+        STAMP_BEGIN();
 
         // ================= feedback: QP (Riccati interior point) =================
         // cold start
@@ -262,8 +299,10 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
         }
         __syncthreads();
         int qstat = AC_MAXITER, qit = 0;
+        STAMP_END(1);
         for (;; ++qit) {
             // ---- residuals
+            STAMP_BEGIN();
             double rs = 0.0, re = 0.0, ri = 0.0, comp = 0.0;
             if (lane <= N) {
                 const int k = lane;
@@ -325,11 +364,13 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
             __syncthreads();
+            STAMP_END(2);
 
             double alpha = 1.0;
             double sigma_mu = 0.0;
             for (int phase = 0; phase < 2; ++phase) {
                 // ---- barrier Hessian terms (predictor only) and Newton gradient q
+                STAMP_BEGIN();
                 if (lane <= N) {
                     const int k = lane;
                     double qk[NZ], dzk[NZ];
@@ -378,7 +419,9 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
                     }
                 }
                 __syncthreads();
+                STAMP_END(3);
                 // ---- Riccati factorisation (predictor only; the corrector reuses it)
+                STAMP_BEGIN();
                 if (phase == 0) {
                     if (lane < NX * NX) {
                         const int i = lane / NX, j = lane % NX;
@@ -433,87 +476,147 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
                     }
                     if (S.flag) { qstat = AC_NAN; break; }
                 }
-                // ---- vector pass (every lane runs the same recursion)
+                STAMP_END(4);
+                // ---- vector + forward passes.  Lane k owns stage k: it folds its
+                // stage block into two affine 5-vector recursions
+                //   p_k = h_k + G_k p_{k+1}          (cost-to-go gradient)
+                //   dx_{k+1} = Phi_k dx_k + e_k        (closed-loop rollout, Phi_k = G_k')
+                // so the sequential chain is one 5x5 mat-vec per stage, carried
+                // in SGPRs through v_readlane; everything else is stage-parallel.
+                STAMP_BEGIN();
                 {
-                    double pp[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) pp[i] = S.q[N][NU + i];
-                    if (lane == 0) {
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) S.p[N][i] = pp[i];
-                    }
-                    for (int k = N - 1; k >= 0; --k) {
-                        double rr[NX], vv[NX];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) rr[i] = S.rdyn[k][i];
+                    const bool own = lane < N;
+                    const int k = own ? lane : 0;
+                    double Fl[NX][NZ], P1[NX][NX], G[NX][NX], hv[NX], W0[NX], W1[NX], Y0[NX], Y1[NX], rr[NX];
+                    const double l00 = S.Lc[k][0], l10 = S.Lc[k][1], l11 = S.Lc[k][2];
+                    double y0a, y0b;
+                    {
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = pp[i];
+                            rr[i] = S.rdyn[k][i];
+                            Y0[i] = S.Y[k][0][i];
+                            Y1[i] = S.Y[k][1][i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += S.P[k + 1][i][j] * rr[j];
-                            vv[i] = acc;
+                            for (int j = 0; j < NZ; ++j) Fl[i][j] = S.F[k][i][j];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) P1[i][j] = S.P[k + 1][i][j];
                         }
-                        double m[NZ];
+                        double c[NX], m0[NZ];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double acc = 0.0;
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) acc += P1[i][j] * rr[j];
+                            c[i] = acc;
+                        }
 #pragma unroll
                         for (int i = 0; i < NZ; ++i) {
                             double acc = S.q[k][i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += S.F[k][j][i] * vv[j];
-                            m[i] = acc;
+                            for (int j = 0; j < NX; ++j) acc += Fl[j][i] * c[j];
+                            m0[i] = acc;
                         }
-                        const double l00 = S.Lc[k][0], l10 = S.Lc[k][1], l11 = S.Lc[k][2];
-                        const double y0 = m[0] / l00;
-                        const double y1 = (m[1] - l10 * y0) / l11;
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) pp[i] = m[NU + i] - S.Y[k][0][i] * y0 - S.Y[k][1][i] * y1;
-                        if (lane == 0) {
-                            S.yv[k][0] = y0; S.yv[k][1] = y1;
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) S.p[k][i] = pp[i];
-                        }
-                    }
-                }
-                __syncthreads();
-                // ---- forward pass
-                {
-                    double dx[NX] = {0, 0, 0, 0, 0};
-                    for (int k = 0; k < N; ++k) {
-                        const double l00 = S.Lc[k][0], l10 = S.Lc[k][1], l11 = S.Lc[k][2];
-                        double c0 = S.yv[k][0], c1 = S.yv[k][1];
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) { c0 += S.Y[k][0][j] * dx[j]; c1 += S.Y[k][1][j] * dx[j]; }
-                        const double du1 = -c1 / l11;
-                        const double du0 = (-c0 - l10 * du1) / l00;
-                        if (lane == 0) {
-                            S.ddz[k][0] = du0; S.ddz[k][1] = du1;
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) S.ddz[k][NU + i] = (k == 0) ? 0.0 : dx[i];
-                        }
-                        double dxn[NX];
+                        y0a = m0[0] / l00;
+                        y0b = (m0[1] - l10 * y0a) / l11;
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = S.rdyn[k][i] + S.F[k][i][0] * du0 + S.F[k][i][1] * du1;
+                            hv[i] = m0[NU + i] - Y0[i] * y0a - Y1[i] * y0b;
+                            W0[i] = Fl[i][0] / l00;
+                            W1[i] = (Fl[i][1] - l10 * W0[i]) / l11;
+                        }
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += S.F[k][i][NU + j] * dx[j];
+                        for (int i = 0; i < NX; ++i)
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) G[i][j] = Fl[j][NU + i] - Y0[i] * W0[j] - Y1[i] * W1[j];
+                    }
+                    // backward chain
+                    double pu[NX], pmine[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) { pu[i] = S.q[N][NU + i]; pmine[i] = pu[i]; }
+                    for (int kk = N - 1; kk >= 0; --kk) {
+                        double pn[NX];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double acc = hv[i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) acc += G[i][j] * pu[j];
+                            pn[i] = acc;
+                        }
+                        const bool mine = (lane == kk);
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            pmine[i] = mine ? pu[i] : pmine[i];
+                            pu[i] = readlane_d(pn[i], kk);
+                        }
+                    }
+                    // feedback terms of stage k
+                    const double ya = y0a + W0[0] * pmine[0] + W0[1] * pmine[1] + W0[2] * pmine[2] + W0[3] * pmine[3] + W0[4] * pmine[4];
+                    const double yb = y0b + W1[0] * pmine[0] + W1[1] * pmine[1] + W1[2] * pmine[2] + W1[3] * pmine[3] + W1[4] * pmine[4];
+                    const double kf1 = -yb / l11;
+                    const double kf0 = (-ya - l10 * kf1) / l00;
+                    double K0[NX], K1[NX], e[NX];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) {
+                        K1[j] = -Y1[j] / l11;
+                        K0[j] = (-Y0[j] - l10 * K1[j]) / l00;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        e[i] = rr[i] + Fl[i][0] * kf0 + Fl[i][1] * kf1;
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) G[i][j] = Fl[i][NU + j] + Fl[i][0] * K0[j] + Fl[i][1] * K1[j];  // Phi
+                    }
+                    // forward chain
+                    double dxu[NX] = {0, 0, 0, 0, 0}, dxmine[NX] = {0, 0, 0, 0, 0};
+                    for (int kk = 0; kk < N; ++kk) {
+                        double dn[NX];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double acc = e[i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) acc += G[i][j] * dxu[j];
+                            dn[i] = acc;
+                        }
+                        const bool mine = (lane == kk);
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            dxmine[i] = mine ? dxu[i] : dxmine[i];
+                            dxu[i] = readlane_d(dn[i], kk);
+                        }
+                    }
+                    if (own) {
+                        double du0 = kf0, du1 = kf1, dxn[NX];
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) { du0 += K0[j] * dxmine[j]; du1 += K1[j] * dxmine[j]; }
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double acc = e[i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) acc += G[i][j] * dxmine[j];
                             dxn[i] = acc;
                         }
-                        if (lane < NX) {
-                            double acc = S.p[k + 1][lane];
+                        S.ddz[k][0] = du0;
+                        S.ddz[k][1] = du1;
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += S.P[k + 1][lane][j] * dxn[j];
-                            S.pin[k][lane] = acc;
+                        for (int i = 0; i < NX; ++i) {
+                            S.ddz[k][NU + i] = (k == 0) ? 0.0 : dxmine[i];
+                            double acc = pmine[i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) acc += P1[i][j] * dxn[j];
+                            S.pin[k][i] = acc;
                         }
+                        if (k == N - 1) {
+                            S.ddz[N][0] = 0.0;
+                            S.ddz[N][1] = 0.0;
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) dx[i] = dxn[i];
-                    }
-                    if (lane == 0) {
-                        S.ddz[N][0] = 0.0; S.ddz[N][1] = 0.0;
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) S.ddz[N][NU + i] = dx[i];
+                            for (int i = 0; i < NX; ++i) S.ddz[N][NU + i] = dxn[i];
+                        }
                     }
                 }
                 __syncthreads();
+                STAMP_END(5);
                 // ---- inequality steps and step length
+                STAMP_BEGIN();
                 double amax = 1e300;
                 if (lane < N) {
                     const int k = lane;
@@ -552,10 +655,12 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
                     if (alpha > 1.0) alpha = 1.0;
                 }
                 __syncthreads();
+                STAMP_END(7);
             }
             if (qstat == AC_NAN) break;
             if (alpha < 1e-12) { qstat = AC_MINSTEP; ++qit; break; }
             // ---- update
+            STAMP_BEGIN();
             if (lane <= N) {
                 const int k = lane;
 #pragma unroll
@@ -571,6 +676,7 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
                 }
             }
             __syncthreads();
+            STAMP_END(8);
         }
         __syncthreads();
         qp_status = qstat;
@@ -601,6 +707,7 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
     }
 
     // ---- completeOneIteration (acados_solver_interface.cpp:387-429)
+    STAMP_BEGIN();
     double Lk = 0.0;
     if (lane < N) {
         double zk[NZ], gd[NZ], Hd[NZ][NZ];
@@ -627,6 +734,8 @@ __global__ __launch_bounds__(64) void sqp_kernel(mpcg_problem pr, int batch,
             info_out[(size_t)sol * MPCG_INFO_STRIDE + 3] = 0;
         }
     }
+    STAMP_END(9);
+    STAMP_STORE(stamps, sol);
 }
 
 // ---- planner selection per scene (guidance_constraints.cpp:372-420, 572-590)
@@ -667,13 +776,14 @@ __global__ void select_best_kernel(int n_scenes, int G, int N, const double* __r
 
 // ---- dispatch over compiled instances ------------------------------------
 static thread_local std::string g_err;
+static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG_STAMPS builds only)
 
 template <class C>
 static int launch(const mpcg_problem& pr, int batch, const double* params, const double* warm,
                   const double* xinit, double* xtraj, double* utraj, double* pobj, int* exit_code,
                   int* info, hipStream_t stream) {
     hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, stream, pr, batch, params, warm, xinit,
-                       xtraj, utraj, pobj, exit_code, info);
+                       xtraj, utraj, pobj, exit_code, info, g_stamps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("sqp_kernel launch: ") + hipGetErrorString(e);
@@ -702,6 +812,9 @@ static Fn find_instance(const mpcg_problem& pr) {
 extern "C" {
 
 int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
+
+/* diagnostic builds only: device buffer of batch x 10 u64 phase-cycle sums */
+void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps = dev_ptr; }
 
 const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }
 

@@ -13,7 +13,8 @@ import numpy as np
 from .layouts import Layout
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libmpcg.so")
+# MPCG_LIB selects a diagnostic build (e.g. libmpcg_stamps.so); default the production library
+LIB_PATH = os.environ.get("MPCG_LIB") or os.path.join(PKG, "libmpcg.so")
 
 NX, NU, NVAR = 5, 2, 7
 INFO_STRIDE = 4
