@@ -1,0 +1,63 @@
+"""Scene sharding over GPUs and the gather of winning trajectories
+(SURVEY.md §8e).
+
+Scenes are independent and the G guesses of a scene only meet in the
+per-scene argmin, so scenes are split into contiguous blocks, one per rank,
+with every guess of a scene on the same GPU; the only exchange is one
+all-gather of the per-scene winner records after the batched solve (RCCL over
+xGMI on MI355X; gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+
+def shard(total_scenes: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous block of ceil(total/world) scenes for `rank`: (first, count)."""
+    per = -(-total_scenes // world)
+    first = min(total_scenes, rank * per)
+    return first, max(0, min(total_scenes, first + per) - first)
+
+
+def winner_width(N: int, nx: int = 5, nu: int = 2) -> int:
+    """xtraj (N+1)*nx | utraj N*nu | pobj | planner index"""
+    return (N + 1) * nx + N * nu + 2
+
+
+def winner_records(xtraj, utraj, pobj, best, G, out=None):
+    """Per-scene record of the selected planner (torch tensors, any device).
+    best == -1 (every planner failed) records planner 0, whose exit code the
+    reference returns in that case (guidance_constraints.cpp:429-442), with
+    index -1 kept in the last column."""
+    import torch
+
+    S = best.shape[0]
+    B, N1, nx = xtraj.shape
+    N = N1 - 1
+    nu = utraj.shape[2]
+    w = winner_width(N, nx, nu)
+    if out is None:
+        out = torch.empty((S, w), dtype=xtraj.dtype, device=xtraj.device)
+    flat = torch.arange(S, device=best.device) * G + best.long().clamp(min=0)
+    out[:, :N1 * nx] = xtraj[flat].reshape(S, -1)
+    out[:, N1 * nx:N1 * nx + N * nu] = utraj[flat].reshape(S, -1)
+    out[:, -2] = pobj[flat]
+    out[:, -1] = best.to(xtraj.dtype)
+    return out
+
+
+def gather_winners(records, world: int, out=None, group=None):
+    """All-gather of equally sized per-rank record blocks (one collective)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return records
+    if out is None:
+        out = torch.empty((records.shape[0] * world, records.shape[1]), dtype=records.dtype, device=records.device)
+    if dist.get_backend(group) == "gloo":
+        parts = list(out.chunk(world, 0))
+        dist.all_gather(parts, records.contiguous(), group=group)
+        if parts[0].data_ptr() != out.data_ptr():
+            out.copy_(torch.cat(parts, 0))
+    else:
+        dist.all_gather_into_tensor(out, records.contiguous(), group=group)
+    return out

@@ -1,0 +1,72 @@
+"""Host-side description of the C ABI (include/mpcg.h): the `mpcg_problem`
+struct, the solver options restated from the reference's acados generator
+and the unicycle bounds.  Importable without a GPU and without loading
+libmpcg.so (the CPU tests use it)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .layouts import Layout
+
+NX, NU, NVAR = 5, 2, 7
+INFO_STRIDE = 4
+
+
+class MpcgProblem(C.Structure):
+    """Mirror of `mpcg_problem` (include/mpcg.h)."""
+    _fields_ = [
+        ("N", C.c_int), ("npar", C.c_int),
+        ("n_lin", C.c_int), ("n_ell", C.c_int), ("n_seg", C.c_int),
+        ("i_w_acc", C.c_int), ("i_w_ang", C.c_int), ("i_w_vel", C.c_int), ("i_v_ref", C.c_int),
+        ("i_w_contour", C.c_int), ("i_w_lag", C.c_int),
+        ("i_spline0", C.c_int),
+        ("i_cons_w", C.c_int), ("i_prev_x", C.c_int), ("i_prev_y", C.c_int),
+        ("i_lin0", C.c_int),
+        ("i_disc_r", C.c_int), ("i_disc_off", C.c_int),
+        ("i_ell0", C.c_int),
+        ("dt", C.c_double), ("rk_steps", C.c_int),
+        ("lbu", C.c_double * 2), ("ubu", C.c_double * 2), ("lbx", C.c_double * 5), ("ubx", C.c_double * 5),
+        ("sqp_iters", C.c_int), ("qp_tol", C.c_double), ("qp_iter_max", C.c_int),
+        ("reg_eps", C.c_double), ("qp_mu0", C.c_double), ("qp_thr0", C.c_double),
+        ("res_eq_fail", C.c_double),
+    ]
+
+
+# acados options restated (generate_acados_solver.py:88-173) + our IPM cold start
+DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2)
+# ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
+UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
+UNICYCLE_UB = (2.0, 0.8, 2000.0, 2000.0, 4 * np.pi, 3.0, 10000.0)
+
+
+def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
+    o = dict(DEFAULT_OPTIONS)
+    o.update(opts)
+    pr = MpcgProblem()
+    pr.N, pr.npar = layout.N, layout.npar
+    pr.n_lin, pr.n_ell, pr.n_seg = layout.n_lin, layout.n_ell, layout.n_seg
+    for k, v in layout.index_struct().items():
+        setattr(pr, k, v)
+    pr.dt = o.get("dt", layout.dt)
+    pr.rk_steps = o.get("rk_steps", layout.rk_steps)
+    lb, ub = o.get("lb", UNICYCLE_LB), o.get("ub", UNICYCLE_UB)
+    for i in range(NU):
+        pr.lbu[i], pr.ubu[i] = lb[i], ub[i]
+    for i in range(NX):
+        pr.lbx[i], pr.ubx[i] = lb[NU + i], ub[NU + i]
+    pr.sqp_iters = o.get("sqp_iters", layout.sqp_iters)
+    pr.qp_tol = o["qp_tol"]
+    pr.qp_iter_max = o["qp_iter_max"]
+    pr.reg_eps = o["reg_eps"]
+    pr.qp_mu0 = o["qp_mu0"]
+    pr.qp_thr0 = o["qp_thr0"]
+    pr.res_eq_fail = o["res_eq_fail"]
+    return pr
+
+
+EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_solve_batch_device",
+           "mpcg_solve_batch_host", "mpcg_select_best_device")
+
+

@@ -1,0 +1,155 @@
+"""Pin the CPU oracle against the reference's own problem definition.
+
+Golden vectors: tests/golden/stage_{C1,C2}.npz, produced by
+tests/golden/gen_golden.py from the reference's Python modules
+(solver_generator/ + mpc_planner_modules/scripts/) through a sympy stand-in
+for casadi.  Parameter maps: tests/golden/parameter_maps.json from the
+reference's `define_parameters` (solver_definition.py:5-16).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oscar_mpc_planner_mr_modification_amd.layouts import config_layout, tmpc_layout
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def maps():
+    with open(os.path.join(GOLDEN, "parameter_maps.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+def test_layout_matches_reference_parameter_map(maps, cfg):
+    lay = config_layout(cfg)
+    assert lay.pmap == maps[cfg]
+    assert lay.npar == {"C1": 98, "C2": 138, "C4": 178}[cfg]   # SURVEY.md §8 dims
+
+
+def test_layout_without_consistency(maps):
+    lay = tmpc_layout(N=20, max_obstacles=4, consistency=False)
+    assert lay.pmap == maps["C1_no_consistency"]
+
+
+def test_reference_known_answer_counts(maps):
+    """solver_generator/test/test_control_modules.py:53-54 and :86-87"""
+    assert len(maps["contouring10_pathrefvel"]) == 10 * 9 + 2 + 4 + 10 * 4
+    assert len(maps["ellipsoid1"]) == 7 + 2
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C1"])
+def test_stage_functions_match_golden(oracle_mod, cfg):
+    lay = config_layout(cfg)
+    o = oracle_mod.Oracle(lay)
+    d = np.load(os.path.join(GOLDEN, f"stage_{cfg}.npz"))
+    for i in range(len(d["z"])):
+        z, p = d["z"][i], d["p"][i]
+        L, g, H = o.stage_cost(z, p)
+        np.testing.assert_allclose(L, d["L"][i], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(g, d["dL"][i], rtol=1e-11, atol=1e-11)
+        np.testing.assert_allclose(H, d["d2L"][i], rtol=1e-10, atol=1e-10)
+        h, J, Hh = o.stage_constraints(z, p)
+        np.testing.assert_allclose(h, d["h"][i], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(J, d["dh"][i], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(Hh, d["d2h"][i], rtol=1e-12, atol=1e-12)
+        f, Jf, Hf = o.dynamics(z)
+        np.testing.assert_allclose(f, d["f"][i], rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(Jf, d["df"][i], rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(Hf, d["d2f"][i], rtol=1e-14, atol=1e-14)
+    lh, uh = o.h_bounds()
+    np.testing.assert_array_equal(lh, np.clip(d["lh"], -1e15, 1e15))   # generate_acados_solver.py:17-24
+    np.testing.assert_array_equal(uh, np.clip(d["uh"], -1e15, 1e15))
+
+
+def test_model_bounds_match_golden(oracle_mod):
+    from oscar_mpc_planner_mr_modification_amd.native_spec import UNICYCLE_LB, UNICYCLE_UB
+    d = np.load(os.path.join(GOLDEN, "stage_C2.npz"))
+    np.testing.assert_allclose(UNICYCLE_LB, d["model_lb"], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(UNICYCLE_UB, d["model_ub"], rtol=0, atol=1e-15)
+
+
+def test_ellipsoid_known_answer(oracle_mod):
+    """test_control_modules.py:69-103: one obstacle at p[2]=5, p[3]=10 with
+    p[-1]=1 -> constraint value strictly inside [1, inf)."""
+    lay = tmpc_layout(N=20, max_obstacles=1)
+    o = oracle_mod.Oracle(lay)
+    o.pr.n_lin = 0
+    o.pr.i_disc_r, o.pr.i_disc_off, o.pr.i_ell0 = 0, 1, 2
+    p = np.zeros(max(lay.npar, 9))
+    p[2], p[3], p[8] = 5.0, 10.0, 1.0
+    h, _, _ = o.stage_constraints(np.zeros(7), p)
+    assert h.shape == (1,) and 1.0 < h[0] < np.inf
+    assert h[0] == pytest.approx(125.0)
+
+
+def test_erk4_sensitivities_and_exact_hessian_by_finite_differences(oracle_mod):
+    o = oracle_mod.Oracle(config_layout("C2"))
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        z = np.array([rng.uniform(-2, 2), rng.uniform(-.8, .8), rng.uniform(-5, 5), rng.uniform(-5, 5),
+                      rng.uniform(-3, 3), rng.uniform(0, 2.5), rng.uniform(0, 10)])
+        adj = rng.normal(size=5)
+        xn, A, B, H = o.erk4(z, adj)
+        eps = 1e-6
+        J = np.zeros((5, 7))
+        Hfd = np.zeros((7, 7))
+        for i in range(7):
+            e = np.zeros(7)
+            e[i] = eps
+            J[:, i] = (o.erk4(z + e)[0] - o.erk4(z - e)[0]) / (2 * eps)
+            gp = adj @ np.hstack(o.erk4(z + e)[1:][::-1])
+            gm = adj @ np.hstack(o.erk4(z - e)[1:][::-1])
+            Hfd[:, i] = (gp - gm) / (2 * eps)
+        np.testing.assert_allclose(np.hstack([B, A]), J, atol=2e-8)
+        np.testing.assert_allclose(H, Hfd, atol=2e-8)
+        np.testing.assert_allclose(H, H.T, atol=0)
+
+
+def test_erk4_exact_for_linear_heading_and_speed(oracle_mod):
+    """psi and v are integrated exactly (psi' = w, v' = a)."""
+    o = oracle_mod.Oracle(config_layout("C2"))
+    z = np.array([0.7, -0.3, 1.0, 2.0, 0.4, 1.5, 3.0])
+    xn, A, B = o.erk4(z)
+    assert xn[2] == pytest.approx(0.4 - 0.3 * 0.2, abs=1e-15)
+    assert xn[3] == pytest.approx(1.5 + 0.7 * 0.2, abs=1e-15)
+
+
+def test_mirror_regularisation(oracle_mod):
+    """acados MIRROR: eigenvalues d -> eps if |d| <= eps else |d|."""
+    o = oracle_mod.Oracle(config_layout("C2"))
+    rng = np.random.default_rng(1)
+    for n in (5, 7):
+        M = rng.normal(size=(n, n))
+        M = M + M.T
+        w, V = np.linalg.eigh(M)
+        w[0] = 3e-5
+        M = V @ np.diag(w) @ V.T
+        f = np.where(np.abs(w) <= 1e-4, 1e-4, np.abs(w))
+        np.testing.assert_allclose(o.mirror(M), V @ np.diag(f) @ V.T, atol=1e-12)
+    np.testing.assert_array_equal(o.mirror(np.zeros((5, 5))), 1e-4 * np.eye(5))
+
+
+def test_oracle_solve_converges_and_is_thread_deterministic(oracle_mod):
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+    lay = config_layout("C2")
+    b = make_batch(lay, 3, 8, seed=11)
+    o = oracle_mod.Oracle(lay)
+    r1 = o.solve_batch(b.params, b.warm, b.xinit, nthreads=1)
+    r8 = o.solve_batch(b.params, b.warm, b.xinit, nthreads=4)
+    np.testing.assert_array_equal(r1["xtraj"], r8["xtraj"])
+    np.testing.assert_array_equal(r1["status"], r8["status"])
+    ok = r1["status"] == 1
+    assert ok.any()
+    # a successful solve is dynamically consistent and respects the input bounds
+    for s in np.where(ok)[0]:
+        xt, ut = r1["xtraj"][s], r1["utraj"][s]
+        assert np.allclose(xt[0], b.xinit[s], atol=1e-12)
+        for k in range(lay.N):
+            xn, _, _ = o.erk4(np.concatenate([ut[k], xt[k]]))
+            assert np.abs(xn - xt[k + 1]).max() < 1e-2
+        assert (ut[:, 0] >= -2 - 1e-6).all() and (ut[:, 0] <= 2 + 1e-6).all()
+        assert (np.abs(ut[:, 1]) <= 0.8 + 1e-6).all()
