@@ -14,7 +14,7 @@ LIB = os.path.join(PKG, "libmpcg.so")
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["mpcg_kernels.hip"]
-HEADERS = ["mpcg_device.h"]
+HEADERS = ["mpcg_device.h", "mpcg_sqp.h"]
 
 
 def _stale(target, deps):
