@@ -5,18 +5,21 @@
 // `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:311-429).
 //
 // Lane layout (PARTS lanes per shooting stage, lane = k * PARTS + part):
-//   part 0 of stage k  cost / ERK4 / MIRROR / Riccati stage algebra of stage k,
-//                      the box-bound rows of stage k, and (PARTS == 2) the
-//                      first h rows
-//   parts 1..          the nonlinear-constraint (h) rows of stage k
-// Every inequality row keeps its interior-point state (bound gap d, slack t,
-// multiplier lambda, predictor product, residual) in REGISTERS of its owner
-// lane for the whole solve; only stage blocks live in LDS (~27 KB per solve
-// for N=20, so 4 solves per CU — one wavefront per SIMD).
-//   element lanes      e < 28 own entry (i >= j) of the 7x7 stage block in the
-//                      Riccati factorisation
+//   part 0 of stage k  cost / ERK4 / MIRROR / stage algebra of stage k and the
+//                      14 box-bound rows (input + state bounds); with PARTS == 2
+//                      also the first h rows
+//   parts >= 1         the nonlinear-constraint (h) rows of stage k, one shared
+//                      code path with a per-lane row offset
+// Every inequality row keeps its interior-point state (slack t, multiplier l,
+// 1/t, residual, predictor product) in REGISTERS of its owner lane for the
+// whole QP; LDS holds only the stage blocks (~37 KB per solve for N=20 ->
+// 4 solves per CU, one wavefront per SIMD).
+//   element lanes      lane e < 28 owns entry (i >= j) of the 7x7 block in the
+//                      Riccati factorisation; the next stage's block is
+//                      prefetched while the current one is reduced
 //   chains             the two 5-vector recursions of each Newton solve run as
-//                      affine maps carried in SGPRs through v_readlane.
+//                      affine maps p_k = h_k + G_k p_{k+1}, dx_{k+1} = G_k' dx_k + e_k
+//                      carried in SGPRs through v_readlane.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -40,20 +43,16 @@ struct Cfg {
     static constexpr int NH = NL + NE;
     static constexpr int PARTS = (64 / (N + 1)) >= 3 ? 3 : 2;
     static_assert((N + 1) * PARTS <= 64, "horizon too long for one wavefront");
-    // h rows owned by part 0 (only when PARTS == 2, to balance the two lanes)
+    // h rows handled by part 0 (PARTS == 2 only, to balance the two lanes)
     static constexpr int H0 = PARTS == 2 ? imax(0, (NH - NBOX) / 2) : 0;
+    // h rows per lane of class 1 (parts >= 1)
+    static constexpr int HC1 = PARTS == 2 ? NH - H0 : (NH + 1) / 2;
+    static constexpr int SLOTS0 = NBOX + H0;
+    static constexpr int SLOTS = imax(SLOTS0, HC1);
+    static constexpr int HSLOTS = imax(H0, HC1);
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
-    // h row range of part p
-    __host__ __device__ static constexpr int hb(int p) {
-        return p == 0 ? 0 : (PARTS == 2 ? H0 : (p == 1 ? 0 : NH / 2));
-    }
-    __host__ __device__ static constexpr int he(int p) {
-        return p == 0 ? H0 : (PARTS == 2 ? NH : (p == 1 ? NH / 2 : NH));
-    }
-    __host__ __device__ static constexpr int nbox(int p) { return p == 0 ? NBOX : 0; }
-    __host__ __device__ static constexpr int nslot(int p) { return nbox(p) + he(p) - hb(p); }
-    static constexpr int SLOTS = imax(nslot(0), imax(nslot(1), PARTS > 2 ? nslot(2) : 0));
-    static constexpr int HSLOTS = imax(he(0) - hb(0), imax(he(1) - hb(1), PARTS > 2 ? he(2) - hb(2) : 0));
+    // first h row of a class-1 lane
+    __host__ __device__ static constexpr int hoff(int part) { return PARTS == 2 ? H0 : (part - 1) * HC1; }
 };
 
 template <class C>
@@ -64,7 +63,7 @@ struct Lds {
     double g[N + 1][NZ];
     double F[N][NX][NZ];      // [B A]
     double b[N][NX];          // shooting defects
-    double dH[N + 1][13];     // barrier terms: diag(7) + (x,y,psi) block (6, packed)
+    double dH[N + 1][13];     // barrier terms: diag(7) + (x,y,psi) block packed xx xy xp yy yp pp
     double q[N + 1][NZ];      // Newton gradient
     double dz[N + 1][NZ];     // QP iterate
     double ddz[N + 1][NZ];    // QP step
@@ -73,13 +72,29 @@ struct Lds {
     double pin[N][NX];
     double rdyn[N][NX];
     double P[N + 1][15];      // Riccati cost-to-go, packed
-    double Lc[N][3];
-    double Y[N][NU][NX];
+    double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
+    double Y[N][NU][NX];      // L^-1 Mux
     double Dg[N][C::NH][3];   // signed h-row gradients on (x, y, psi)
+    double hd[N][C::NH];      // h-row bound gaps (uh - h or h - lh)
     double Msc[28];           // factorisation scratch
     double xinit[NX];
     int flag;
 };
+
+// Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
+// production build compiles them out).  Read shares, not absolute times.
+#ifdef MPCG_STAMPS
+#define STAMP_DECL unsigned long long st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0_ = 0;
+#define STAMP_BEGIN() do { __syncthreads(); st_t0_ = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP_END(i) do { __syncthreads(); st_acc_[i] += __builtin_amdgcn_s_memtime() - st_t0_; } while (0)
+#define STAMP_STORE(ptr, sol) \
+    do { if ((ptr) && threadIdx.x == 0) for (int i_ = 0; i_ < 10; ++i_) (ptr)[(size_t)(sol) * 10 + i_] = st_acc_[i_]; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END(i) do {} while (0)
+#define STAMP_STORE(ptr, sol) do {} while (0)
+#endif
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -89,11 +104,6 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
 }
 __device__ __forceinline__ double wave_sum(double v) {
@@ -107,7 +117,7 @@ __host__ __device__ constexpr int box_var(int s) { return s < 2 * NU ? (s >> 1) 
 __host__ __device__ constexpr double box_sign(int s) { return (s & 1) ? 1.0 : -1.0; }
 
 // barrier contribution at (i, j), i >= j: diagonal part dh[0..6] plus the
-// (x, y, psi) block dh[7..12] packed xx xy xp yy yp pp
+// (x, y, psi) block dh[7..12]
 __device__ __forceinline__ double dh_at(const double* dh, int i, int j) {
     double v = (i == j) ? dh[i] : 0.0;
     if (i >= 2 && i <= 4 && j >= 2 && j <= 4) {
@@ -117,50 +127,62 @@ __device__ __forceinline__ double dh_at(const double* dh, int i, int j) {
     return v;
 }
 
-// Per-lane register state of the inequality rows it owns.
+// Register state of the inequality rows a lane owns (slot s).
 template <class C>
 struct Rows {
-    double d[C::SLOTS], t[C::SLOTS], l[C::SLOTS], rin[C::SLOTS], pr[C::SLOTS];
+    double t[C::SLOTS], l[C::SLOTS], it[C::SLOTS], rin[C::SLOTS], pr[C::SLOTS];
     double nlam[C::HSLOTS];  // NLP multiplier of the h row (Hessian weight of the next linearisation)
 };
 
-// dispatch a generic lambda on the lane's part as a compile-time constant
+// Row-class descriptors: class 0 = part 0 (box rows, then h rows [0, H0));
+// class 1 = parts >= 1 (h rows [hoff, hoff + HC1)).
+template <class C, int CL>
+struct RowClass {
+    static constexpr int NB = CL == 0 ? NBOX : 0;
+    static constexpr int NHR = CL == 0 ? C::H0 : C::HC1;
+    static constexpr int NS = NB + NHR;
+};
+
+// dispatch a generic lambda on the lane's row class (compile-time) + h offset
 template <class C, class Fn>
-__device__ __forceinline__ void on_part(int part, Fn&& fn) {
-    if (part == 0) fn(std::integral_constant<int, 0>{});
-    else if (part == 1) fn(std::integral_constant<int, 1>{});
-    else if constexpr (C::PARTS > 2) {
-        if (part == 2) fn(std::integral_constant<int, 2>{});
-    }
+__device__ __forceinline__ void on_class(int part, Fn&& fn) {
+    if (part == 0) fn(std::integral_constant<int, 0>{}, 0);
+    else fn(std::integral_constant<int, 1>{}, C::hoff(part));
 }
 
-// row s of part P is active at stage k
-template <class C, int P>
-__device__ __forceinline__ bool row_active(int s, int k) {
-    if (s < C::nbox(P)) return (k == 0) ? (s < 2 * NU) : (k < C::N);
-    return k >= 1 && k < C::N;
+// row s of class CL is active at stage k (h rows beyond NH are padding)
+template <class C, int CL>
+__device__ __forceinline__ bool row_active(int s, int k, int hoff) {
+    if (s < RowClass<C, CL>::NB) return (k == 0) ? (s < 2 * NU) : (k < C::N);
+    return k >= 1 && k < C::N && (hoff + s - RowClass<C, CL>::NB) < C::NH;
+}
+
+// D_row . v for row s (v in z-order)
+template <class C, int CL>
+__device__ __forceinline__ double row_dot(const double (*Dg)[3], int s, int hoff, const double v[NZ]) {
+    if (s < RowClass<C, CL>::NB) return box_sign(s) * v[box_var(s)];
+    const int hh = hoff + s - RowClass<C, CL>::NB;
+    return Dg[hh][0] * v[2] + Dg[hh][1] * v[3] + Dg[hh][2] * v[4];
 }
 
 // h values, signed gradients, bound gaps and the multiplier-weighted Hessian
-// (on x, y, psi: xx xy xp yy yp pp) of the h rows [hb(P), he(P)) of stage k.
-template <class C, int P>
+// (xx xy xp yy yp pp on x, y, psi) of the h rows of a lane at stage k.
+template <class C, int CL>
 __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[NZ],
-                                       Rows<C>& R, double hb6[6], double (*Dg)[3]) {
+                                       int hoff, const double* nlam, double hb6[6], double (*Dg)[3], double* hd) {
     const double x = z[2], y = z[3], psi = z[4];
     const double rdisc = pk[pr.i_disc_r], off = pk[pr.i_disc_off];
     double sp, cp;
     sincos(psi, &sp, &cp);
     const double dxp = -off * sp, dyp = off * cp, dxpp = -off * cp, dypp = -off * sp;
 #pragma unroll
-    for (int hh = C::hb(P); hh < C::he(P); ++hh) {
-        constexpr int base = C::nbox(P);
-        const int s = base + hh - C::hb(P);
-        const int hs = hh - C::hb(P);
+    for (int r = 0; r < RowClass<C, CL>::NHR; ++r) {
+        const int hh = hoff + r;
+        if (hh >= C::NH) continue;
         if (hh < C::NL) {
             // topology halfspace a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370)
             const double* c = pk + pr.i_lin0 + 3 * hh;
-            const double h = c[0] * x + c[1] * y - c[2];
-            R.d[s] = 0.0 - h;
+            hd[hh] = 0.0 - (c[0] * x + c[1] * y - c[2]);
             Dg[hh][0] = c[0];
             Dg[hh][1] = c[1];
             Dg[hh][2] = 0.0;
@@ -178,12 +200,11 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             const double M11 = so * so * D0 + co * co * D1;
             const double ddx = x + off * cp - o[0], ddy = y + off * sp - o[1];
             const double Mdx = M00 * ddx + M01 * ddy, Mdy = M01 * ddx + M11 * ddy;
-            const double h = ddx * Mdx + ddy * Mdy;
-            R.d[s] = h - 1.0;
+            hd[hh] = (ddx * Mdx + ddy * Mdy) - 1.0;
             Dg[hh][0] = -2.0 * Mdx;
             Dg[hh][1] = -2.0 * Mdy;
             Dg[hh][2] = -2.0 * (Mdx * dxp + Mdy * dyp);
-            const double wgt = -R.nlam[hs];  // lower-bound row: Hessian weight -lambda
+            const double wgt = -nlam[r];  // lower-bound row: Hessian weight -lambda
             if (wgt != 0.0) {
                 const double hxp = 2.0 * (M00 * dxp + M01 * dyp);
                 const double hyp = 2.0 * (M01 * dxp + M11 * dyp);
@@ -196,12 +217,24 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
     }
 }
 
+// bound gap of row s at stage k (box rows from the iterate, h rows from LDS)
+template <class C, int CL>
+__device__ __forceinline__ double row_gap(const mpcg_problem& pr, const double* zk, const double* hd, int s, int hoff) {
+    if (s < RowClass<C, CL>::NB) {
+        const int v = box_var(s);
+        const double lo = v < NU ? pr.lbu[v] : pr.lbx[v - NU];
+        const double hi = v < NU ? pr.ubu[v] : pr.ubx[v - NU];
+        return (s & 1) ? hi - zk[v] : zk[v] - lo;
+    }
+    return hd[hoff + s - RowClass<C, CL>::NB];
+}
+
 template <class C>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, const double* __restrict__ params,
-                                                 const double* __restrict__ warm, const double* __restrict__ xinit,
-                                                 double* __restrict__ xtraj, double* __restrict__ utraj,
-                                                 double* __restrict__ pobj_out, int* __restrict__ exit_out,
-                                                 int* __restrict__ info_out, unsigned long long* __restrict__ stamps) {
+                                                    const double* __restrict__ warm, const double* __restrict__ xinit,
+                                                    double* __restrict__ xtraj, double* __restrict__ utraj,
+                                                    double* __restrict__ pobj_out, int* __restrict__ exit_out,
+                                                    int* __restrict__ info_out, unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, PARTS = C::PARTS;
     __shared__ Lds<C> S;
     const int sol = blockIdx.x;
@@ -210,11 +243,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     const int k = lane / PARTS;          // my stage
     const int part = lane - k * PARTS;   // my part
     const bool stage_lane = (part == 0) && (k <= N);
-    const int kc = k < N ? k : N - 1;    // clamped stage for parameter / F access
+    const int ks = k <= N ? k : N;       // clamped stage (always a valid LDS index)
+    const int kc = k < N ? k : N - 1;    // clamped stage < N
     const int npar = pr.npar;
     const double* pbase = params + (size_t)sol * N * npar;
     const double* pk = pbase + (size_t)kc * npar;
     (void)stamps;
+    STAMP_DECL
 
     Rows<C> R;
 #pragma unroll
@@ -234,86 +269,91 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
     for (int it = 0; it < pr.sqp_iters; ++it) {
         // =============== preparation: linearise every stage ===============
-        double zk[NZ];
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) zk[i] = S.z[k <= N ? k : N][i];
-        double hb6[6] = {0, 0, 0, 0, 0, 0};
-        if (k >= 1 && k < N) {
-            on_part<C>(part, [&](auto Pc) {
-                constexpr int P = decltype(Pc)::value;
-                h_rows<C, P>(pr, pk, zk, R, hb6, S.Dg[k]);
-            });
-        }
-        // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
+        STAMP_BEGIN();
         {
-            double acc[6];
+            double zk[NZ];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) acc[i] = hb6[i];
+            for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
+            double hb6[6] = {0, 0, 0, 0, 0, 0};
+            if (k >= 1 && k < N) {
+                on_class<C>(part, [&](auto Cc, int hoff) {
+                    constexpr int CL = decltype(Cc)::value;
+                    if constexpr (RowClass<C, CL>::NHR > 0)
+                        h_rows<C, CL>(pr, pk, zk, hoff, R.nlam, hb6, S.Dg[k], S.hd[k]);
+                });
+            }
+            // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
+            {
+                double acc[6];
 #pragma unroll
-            for (int p = 1; p < PARTS; ++p)
+                for (int i = 0; i < 6; ++i) acc[i] = hb6[i];
 #pragma unroll
-                for (int i = 0; i < 6; ++i) acc[i] += __shfl_down(hb6[i], p);
+                for (int p = 1; p < PARTS; ++p)
 #pragma unroll
-            for (int i = 0; i < 6; ++i) hb6[i] = acc[i];
+                    for (int i = 0; i < 6; ++i) acc[i] += __shfl_down(hb6[i], p);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) hb6[i] = acc[i];
+            }
+            double resl = 0.0;
+            if (stage_lane && k < N) {
+                double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
+                stage_cost(pr, pk, zk, g, H, true);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
+                erk_unicycle(pr, zk, pi, xn, F, H);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    const double bi = xn[i] - S.z[k + 1][NU + i];
+                    S.b[k][i] = bi;
+                    resl = fmax(resl, fabs(bi));
+#pragma unroll
+                    for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                }
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) S.g[k][i] = g[i];
+                H[2][2] += hb6[0]; H[2][3] += hb6[1]; H[3][2] += hb6[1];
+                H[2][4] += hb6[2]; H[4][2] += hb6[2];
+                H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
+                H[4][4] += hb6[5];
+                mirror7(H, pr.reg_eps);
+#pragma unroll
+                for (int i = 0; i < NZ; ++i)
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) S.H[k][sym(i, j)] = H[i][j];
+            } else if (stage_lane && k == N) {
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) {
+                    S.g[N][i] = 0.0;
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) S.H[N][sym(i, j)] = (i == j && i >= NU) ? pr.reg_eps : 0.0;
+                }
+            }
+            res_eq = wave_max(resl);
+            if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
         }
-        double resl = 0.0;
-        if (stage_lane && k < N) {
-            double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
-            stage_cost(pr, pk, zk, g, H, true);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
-            erk_unicycle(pr, zk, pi, xn, F, H);
-            H[2][2] += hb6[0]; H[2][3] += hb6[1]; H[3][2] += hb6[1];
-            H[2][4] += hb6[2]; H[4][2] += hb6[2];
-            H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
-            H[4][4] += hb6[5];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                const double bi = xn[i] - S.z[k + 1][NU + i];
-                S.b[k][i] = bi;
-                resl = fmax(resl, fabs(bi));
-#pragma unroll
-                for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
-            }
-            // box rows: input bounds on every stage < N, state bounds on 1..N-1
-#pragma unroll
-            for (int s = 0; s < NBOX; ++s) {
-                const int v = box_var(s);
-                const double lo = v < NU ? pr.lbu[v] : pr.lbx[v - NU];
-                const double hi = v < NU ? pr.ubu[v] : pr.ubx[v - NU];
-                R.d[s] = (s & 1) ? hi - zk[v] : zk[v] - lo;
-            }
-            mirror7(H, pr.reg_eps);
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) {
-                S.g[k][i] = g[i];
-#pragma unroll
-                for (int j = 0; j <= i; ++j) S.H[k][sym(i, j)] = H[i][j];
-            }
-        } else if (stage_lane && k == N) {
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) {
-                S.g[N][i] = 0.0;
-#pragma unroll
-                for (int j = 0; j <= i; ++j) S.H[N][sym(i, j)] = (i == j && i >= NU) ? pr.reg_eps : 0.0;
-            }
-        }
-        res_eq = wave_max(resl);
-        if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
         __syncthreads();
+        STAMP_END(0);
 
         // =============== feedback: QP by Riccati interior point ===============
-        // cold start
-        on_part<C>(part, [&](auto Pc) {
-            constexpr int P = decltype(Pc)::value;
+        STAMP_BEGIN();
+        // cold start: t = max(gap, thr0), l = mu0 / t
+        {
+            double zk[NZ];
 #pragma unroll
-            for (int s = 0; s < C::nslot(P); ++s) {
-                const double t0 = R.d[s] > pr.qp_thr0 ? R.d[s] : pr.qp_thr0;
-                R.t[s] = t0;
-                R.l[s] = pr.qp_mu0 / t0;
-                R.pr[s] = 0.0;
-            }
-        });
+            for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
+            on_class<C>(part, [&](auto Cc, int hoff) {
+                constexpr int CL = decltype(Cc)::value;
+#pragma unroll
+                for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                    if (!row_active<C, CL>(s, k, hoff)) continue;
+                    const double gap = row_gap<C, CL>(pr, zk, S.hd[kc], s, hoff);
+                    const double t0 = gap > pr.qp_thr0 ? gap : pr.qp_thr0;
+                    R.t[s] = t0;
+                    R.l[s] = pr.qp_mu0 / t0;
+                    R.pr[s] = 0.0;
+                }
+            });
+        }
         if (stage_lane) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i)
@@ -324,80 +364,79 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             }
         }
         __syncthreads();
+        STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
         double Hdz[NZ];  // part 0: H_k dz_k of the current iterate
         for (;; ++qit) {
             // ---- residuals
-            double dzk[NZ];
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) dzk[i] = S.dz[k <= N ? k : N][i];
+            STAMP_BEGIN();
             double rs = 0.0, re = 0.0, ri = 0.0, comp = 0.0;
-            double rbox[NZ] = {0, 0, 0, 0, 0, 0, 0}, rh[3] = {0, 0, 0};
-            if (k <= N) {
-                on_part<C>(part, [&](auto Pc) {
-                    constexpr int P = decltype(Pc)::value;
+            {
+                double zk[NZ], dzk[NZ];
 #pragma unroll
-                    for (int s = 0; s < C::nslot(P); ++s) {
-                        if (!row_active<C, P>(s, k)) continue;
-                        double dot;
-                        if (s < C::nbox(P)) {
-                            dot = box_sign(s) * dzk[box_var(s)];
-                            rbox[box_var(s)] += box_sign(s) * R.l[s];
+                for (int i = 0; i < NZ; ++i) { dzk[i] = S.dz[ks][i]; zk[i] = S.z[ks][i]; }
+                double rbox[NZ] = {0, 0, 0, 0, 0, 0, 0}, rh[3] = {0, 0, 0};
+                on_class<C>(part, [&](auto Cc, int hoff) {
+                    constexpr int CL = decltype(Cc)::value;
+#pragma unroll
+                    for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                        if (!row_active<C, CL>(s, k, hoff)) continue;
+                        const double l = R.l[s], t = R.t[s];
+                        if (s < RowClass<C, CL>::NB) {
+                            rbox[box_var(s)] += box_sign(s) * l;
                         } else {
-                            const int hh = C::hb(P) + s - C::nbox(P);
-                            const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
-                            dot = a * dzk[2] + bq * dzk[3] + c * dzk[4];
-                            rh[0] += a * R.l[s]; rh[1] += bq * R.l[s]; rh[2] += c * R.l[s];
+                            const int hh = hoff + s - RowClass<C, CL>::NB;
+                            rh[0] += S.Dg[k][hh][0] * l; rh[1] += S.Dg[k][hh][1] * l; rh[2] += S.Dg[k][hh][2] * l;
                         }
-                        const double rin = dot + R.t[s] - R.d[s];
+                        const double rin = row_dot<C, CL>(S.Dg[kc], s, hoff, dzk) + t -
+                                           row_gap<C, CL>(pr, zk, S.hd[kc], s, hoff);
                         R.rin[s] = rin;
+                        R.it[s] = 1.0 / t;
                         ri = fmax(ri, fabs(rin));
-                        comp += R.l[s] * R.t[s];
+                        comp += l * t;
                     }
                 });
-            }
-            {
                 double acc[3] = {rh[0], rh[1], rh[2]};
 #pragma unroll
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
                     for (int i = 0; i < 3; ++i) acc[i] += __shfl_down(rh[i], p);
                 rbox[2] += acc[0]; rbox[3] += acc[1]; rbox[4] += acc[2];
-            }
-            if (stage_lane) {
-                double r[NZ];
+                if (stage_lane) {
+                    double r[NZ];
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) {
-                    double acc = 0.0;
+                    for (int i = 0; i < NZ; ++i) {
+                        double a = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NZ; ++j) acc += S.H[k][sym(i, j)] * dzk[j];
-                    Hdz[i] = acc;
-                    r[i] = acc + S.g[k][i] + rbox[i];
-                }
-                if (k < N) {
+                        for (int j = 0; j < NZ; ++j) a += S.H[k][sym(i, j)] * dzk[j];
+                        Hdz[i] = a;
+                        r[i] = a + S.g[k][i] + rbox[i];
+                    }
+                    if (k < N) {
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) {
-                        const double pm = S.piq[k][m];
+                        for (int m = 0; m < NX; ++m) {
+                            const double pm = S.piq[k][m];
 #pragma unroll
-                        for (int i = 0; i < NZ; ++i) r[i] += S.F[k][m][i] * pm;
+                            for (int i = 0; i < NZ; ++i) r[i] += S.F[k][m][i] * pm;
+                        }
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double a = S.b[k][i] - S.dz[k + 1][NU + i];
+#pragma unroll
+                            for (int j = 0; j < NZ; ++j) a += S.F[k][i][j] * dzk[j];
+                            S.rdyn[k][i] = a;
+                            re = fmax(re, fabs(a));
+                        }
+                    }
+                    if (k > 0) {
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) r[NU + i] -= S.piq[k - 1][i];
                     }
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        double acc = S.b[k][i] - S.dz[k + 1][NU + i];
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) acc += S.F[k][i][j] * dzk[j];
-                        S.rdyn[k][i] = acc;
-                        re = fmax(re, fabs(acc));
+                    for (int i = 0; i < NZ; ++i) {
+                        const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
+                        if (free_var) rs = fmax(rs, fabs(r[i]));
                     }
-                }
-                if (k > 0) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) r[NU + i] -= S.piq[k - 1][i];
-                }
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) {
-                    const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
-                    if (free_var) rs = fmax(rs, fabs(r[i]));
                 }
             }
             rs = wave_max(rs);
@@ -409,36 +448,38 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
             __syncthreads();
+            STAMP_END(2);
 
             double alpha = 1.0, sigma_mu = 0.0;
             for (int phase = 0; phase < 2; ++phase) {
                 // ---- barrier terms + Newton gradient
+                STAMP_BEGIN();
                 {
                     double qb[NZ] = {0, 0, 0, 0, 0, 0, 0}, dd[NZ] = {0, 0, 0, 0, 0, 0, 0};
                     double qh[3] = {0, 0, 0}, dbh[6] = {0, 0, 0, 0, 0, 0};
-                    if (k <= N) {
-                        on_part<C>(part, [&](auto Pc) {
-                            constexpr int P = decltype(Pc)::value;
+                    on_class<C>(part, [&](auto Cc, int hoff) {
+                        constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                            for (int s = 0; s < C::nslot(P); ++s) {
-                                if (!row_active<C, P>(s, k)) continue;
-                                const double l = R.l[s], t = R.t[s];
-                                const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
-                                const double coef = l + (l * R.rin[s] - rc) / t;
-                                const double wgt = l / t;
-                                if (s < C::nbox(P)) {
-                                    qb[box_var(s)] += box_sign(s) * coef;
-                                    dd[box_var(s)] += wgt;
-                                } else {
-                                    const int hh = C::hb(P) + s - C::nbox(P);
-                                    const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
-                                    qh[0] += a * coef; qh[1] += bq * coef; qh[2] += c * coef;
+                        for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                            if (!row_active<C, CL>(s, k, hoff)) continue;
+                            const double l = R.l[s], t = R.t[s], itt = R.it[s];
+                            const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
+                            const double coef = l + (l * R.rin[s] - rc) * itt;
+                            const double wgt = l * itt;
+                            if (s < RowClass<C, CL>::NB) {
+                                qb[box_var(s)] += box_sign(s) * coef;
+                                dd[box_var(s)] += wgt;
+                            } else {
+                                const int hh = hoff + s - RowClass<C, CL>::NB;
+                                const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
+                                qh[0] += a * coef; qh[1] += bq * coef; qh[2] += c * coef;
+                                if (phase == 0) {
                                     dbh[0] += a * wgt * a; dbh[1] += a * wgt * bq; dbh[2] += a * wgt * c;
                                     dbh[3] += bq * wgt * bq; dbh[4] += bq * wgt * c; dbh[5] += c * wgt * c;
                                 }
                             }
-                        });
-                    }
+                        }
+                    });
                     double aq[3] = {qh[0], qh[1], qh[2]}, ab[6];
 #pragma unroll
                     for (int i = 0; i < 6; ++i) ab[i] = dbh[i];
@@ -464,115 +505,115 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     }
                 }
                 __syncthreads();
+                STAMP_END(3);
                 // ---- Riccati factorisation (predictor only; the corrector reuses it)
+                STAMP_BEGIN();
                 if (phase == 0) {
-                    if (lane < 15) {
-                        int i = 0;
-                        while ((i + 1) * (i + 2) / 2 <= lane) ++i;
-                        const int j = lane - i * (i + 1) / 2;
-                        S.P[N][lane] = S.H[N][sym(NU + i, NU + j)] + dh_at(S.dH[N], NU + i, NU + j);
-                    }
-                    if (lane == 0) S.flag = 0;
                     // element lane -> (ei, ej), ei >= ej, of the 7x7 block
                     int ei = 0;
-                    if (lane < 28) {
-                        while ((ei + 1) * (ei + 2) / 2 <= lane) ++ei;
-                    }
+                    while ((ei + 1) * (ei + 2) / 2 <= lane && ei < 6) ++ei;
                     const int ej = lane < 28 ? lane - ei * (ei + 1) / 2 : 0;
-                    // barrier terms of entry (ei, ej): diagonal part and (x,y,psi) block part
                     const int dhd = (ei == ej) ? ei : -1;
                     int dhb = -1;
                     if (ei >= 2 && ei <= 4 && ej >= 2 && ej <= 4) {
                         const int a = ei - 2, c = ej - 2;
                         dhb = NZ + ((c == 0) ? a : (c == 1 ? 2 + a : 5));
                     }
+                    // P lanes: (pi_, pj_) of the 5x5 block
+                    int pi_ = 0;
+                    while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < 4) ++pi_;
+                    const int pj_ = lane < 15 ? lane - pi_ * (pi_ + 1) / 2 : 0;
+                    if (lane < 15) S.P[N][lane] = S.H[N][sym(NU + pi_, NU + pj_)] + dh_at(S.dH[N], NU + pi_, NU + pj_);
+                    if (lane == 0) S.flag = 0;
                     __syncthreads();
+                    // prefetch of stage N-1's block
+                    const int le = lane < 28 ? lane : 0;
+                    double fi[NX], fj[NX], hv;
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) { fi[m] = S.F[N - 1][m][ei]; fj[m] = S.F[N - 1][m][ej]; }
+                    hv = S.H[N - 1][le] + (dhd >= 0 ? S.dH[N - 1][dhd] : 0.0) + (dhb >= 0 ? S.dH[N - 1][dhb] : 0.0);
                     for (int kk = N - 1; kk >= 0; --kk) {
-                        if (lane < 28) {
-                            double Pm[15];
+                        double Pm[15];
 #pragma unroll
-                            for (int e = 0; e < 15; ++e) Pm[e] = S.P[kk + 1][e];
-                            double fi[NX], fj[NX];
+                        for (int e = 0; e < 15; ++e) Pm[e] = S.P[kk + 1][e];
+                        double v = hv;
 #pragma unroll
-                            for (int m = 0; m < NX; ++m) { fi[m] = S.F[kk][m][ei]; fj[m] = S.F[kk][m][ej]; }
-                            double v = S.H[kk][lane] + (dhd >= 0 ? S.dH[kk][dhd] : 0.0) + (dhb >= 0 ? S.dH[kk][dhb] : 0.0);
+                        for (int m = 0; m < NX; ++m) {
+                            double tm = 0.0;
 #pragma unroll
-                            for (int m = 0; m < NX; ++m) {
-                                double tm = 0.0;
-#pragma unroll
-                                for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
-                                v += fi[m] * tm;
-                            }
-                            S.Msc[lane] = v;
+                            for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
+                            v += fi[m] * tm;
                         }
+                        if (lane < 28) S.Msc[lane] = v;
+                        // prefetch the next (lower) stage while this one is reduced
+                        const int kn = kk > 0 ? kk - 1 : 0;
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) { fi[m] = S.F[kn][m][ei]; fj[m] = S.F[kn][m][ej]; }
+                        hv = S.H[kn][le] + (dhd >= 0 ? S.dH[kn][dhd] : 0.0) + (dhb >= 0 ? S.dH[kn][dhb] : 0.0);
                         __syncthreads();
                         if (lane < 15) {
-                            int i = 0;
-                            while ((i + 1) * (i + 2) / 2 <= lane) ++i;
-                            const int j = lane - i * (i + 1) / 2;
                             const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
                             const double l00 = sqrt(m00);
-                            const double l10 = m10 / l00;
+                            const double il00 = 1.0 / l00;
+                            const double l10 = m10 * il00;
                             const double r11 = m11 - l10 * l10;
                             const double l11 = sqrt(r11);
+                            const double il11 = 1.0 / l11;
                             if (!(m00 > 0.0) || !(r11 > 0.0)) S.flag = 1;
-                            const double y0i = S.Msc[sym(NU + i, 0)] / l00;
-                            const double y1i = (S.Msc[sym(NU + i, 1)] - l10 * y0i) / l11;
-                            const double y0j = S.Msc[sym(NU + j, 0)] / l00;
-                            const double y1j = (S.Msc[sym(NU + j, 1)] - l10 * y0j) / l11;
-                            S.P[kk][lane] = S.Msc[sym(NU + i, NU + j)] - y0i * y0j - y1i * y1j;
-                            if (j == 0) { S.Y[kk][0][i] = y0i; S.Y[kk][1][i] = y1i; }
-                            if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = l11; }
+                            const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
+                            const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
+                            const double y0j = S.Msc[sym(NU + pj_, 0)] * il00;
+                            const double y1j = (S.Msc[sym(NU + pj_, 1)] - l10 * y0j) * il11;
+                            S.P[kk][lane] = S.Msc[sym(NU + pi_, NU + pj_)] - y0i * y0j - y1i * y1j;
+                            if (pj_ == 0) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
+                            if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
                         }
                         __syncthreads();
                     }
                     if (S.flag) { qstat = AC_NAN; break; }
                 }
+                STAMP_END(4);
                 // ---- vector + forward passes: affine 5-vector recursions in SGPRs
+                STAMP_BEGIN();
                 {
                     const bool own = stage_lane && k < N;
                     const int kq = own ? k : 0;
-                    double Fl[NX][NZ], P1[15], G[NX][NX], hv[NX], W0[NX], W1[NX], Y0[NX], Y1[NX], rr[NX];
-                    const double l00 = S.Lc[kq][0], l10 = S.Lc[kq][1], l11 = S.Lc[kq][2];
-                    double y0a, y0b;
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        rr[i] = S.rdyn[kq][i];
-                        Y0[i] = S.Y[kq][0][i];
-                        Y1[i] = S.Y[kq][1][i];
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) Fl[i][j] = S.F[kq][i][j];
-                    }
-#pragma unroll
-                    for (int e = 0; e < 15; ++e) P1[e] = S.P[kq + 1][e];
+                    const double l10 = S.Lc[kq][1], il00 = S.Lc[kq][2], il11 = S.Lc[kq][3];
+                    double G[NX][NX], hv[NX], W0[NX], W1[NX], y0a, y0b;
                     {
-                        double c[NX], m0[NZ];
+                        double c[NX], rr[NX];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rr[i] = S.rdyn[kq][i];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = 0.0;
+                            double a = 0.0;
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += P1[sym(i, j)] * rr[j];
-                            c[i] = acc;
+                            for (int j = 0; j < NX; ++j) a += S.P[kq + 1][sym(i, j)] * rr[j];
+                            c[i] = a;
                         }
+                        double m0[NZ];
 #pragma unroll
                         for (int i = 0; i < NZ; ++i) {
-                            double acc = S.q[kq][i];
+                            double a = S.q[kq][i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += Fl[j][i] * c[j];
-                            m0[i] = acc;
+                            for (int j = 0; j < NX; ++j) a += S.F[kq][j][i] * c[j];
+                            m0[i] = a;
                         }
-                        y0a = m0[0] / l00;
-                        y0b = (m0[1] - l10 * y0a) / l11;
+                        y0a = m0[0] * il00;
+                        y0b = (m0[1] - l10 * y0a) * il11;
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            hv[i] = m0[NU + i] - Y0[i] * y0a - Y1[i] * y0b;
-                            W0[i] = Fl[i][0] / l00;
-                            W1[i] = (Fl[i][1] - l10 * W0[i]) / l11;
+                            const double Y0 = S.Y[kq][0][i], Y1 = S.Y[kq][1][i];
+                            hv[i] = m0[NU + i] - Y0 * y0a - Y1 * y0b;
+                            W0[i] = S.F[kq][i][0] * il00;
+                            W1[i] = (S.F[kq][i][1] - l10 * W0[i]) * il11;
                         }
 #pragma unroll
-                        for (int i = 0; i < NX; ++i)
+                        for (int i = 0; i < NX; ++i) {
+                            const double Y0 = S.Y[kq][0][i], Y1 = S.Y[kq][1][i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) G[i][j] = Fl[j][NU + i] - Y0[i] * W0[j] - Y1[i] * W1[j];
+                            for (int j = 0; j < NX; ++j) G[i][j] = S.F[kq][j][NU + i] - Y0 * W0[j] - Y1 * W1[j];
+                        }
                     }
                     double pu[NX], pmine[NX];
 #pragma unroll
@@ -581,10 +622,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         double pn[NX];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = hv[i];
+                            double a = hv[i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += G[i][j] * pu[j];
-                            pn[i] = acc;
+                            for (int j = 0; j < NX; ++j) a += G[i][j] * pu[j];
+                            pn[i] = a;
                         }
                         const bool mine = (k == kk) && (part == 0);
 #pragma unroll
@@ -593,33 +634,25 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             pu[i] = readlane_d(pn[i], kk * PARTS);
                         }
                     }
+                    // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
                     const double ya = y0a + W0[0] * pmine[0] + W0[1] * pmine[1] + W0[2] * pmine[2] + W0[3] * pmine[3] +
                                       W0[4] * pmine[4];
                     const double yb = y0b + W1[0] * pmine[0] + W1[1] * pmine[1] + W1[2] * pmine[2] + W1[3] * pmine[3] +
                                       W1[4] * pmine[4];
-                    const double kf1 = -yb / l11;
-                    const double kf0 = (-ya - l10 * kf1) / l00;
-                    double K0[NX], K1[NX], e[NX];
+                    const double kf1 = -yb * il11;
+                    const double kf0 = (-ya - l10 * kf1) * il00;
+                    double e[NX];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) {
-                        K1[j] = -Y1[j] / l11;
-                        K0[j] = (-Y0[j] - l10 * K1[j]) / l00;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        e[i] = rr[i] + Fl[i][0] * kf0 + Fl[i][1] * kf1;
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) G[i][j] = Fl[i][NU + j] + Fl[i][0] * K0[j] + Fl[i][1] * K1[j];
-                    }
+                    for (int i = 0; i < NX; ++i) e[i] = S.rdyn[kq][i] + S.F[kq][i][0] * kf0 + S.F[kq][i][1] * kf1;
                     double dxu[NX] = {0, 0, 0, 0, 0}, dxmine[NX] = {0, 0, 0, 0, 0};
                     for (int kk = 0; kk < N; ++kk) {
                         double dn[NX];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = e[i];
+                            double a = e[i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += G[i][j] * dxu[j];
-                            dn[i] = acc;
+                            for (int j = 0; j < NX; ++j) a += G[j][i] * dxu[j];
+                            dn[i] = a;
                         }
                         const bool mine = (k == kk) && (part == 0);
 #pragma unroll
@@ -629,25 +662,30 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     if (own) {
-                        double du0 = kf0, du1 = kf1, dxn[NX];
+                        double du1 = kf1, du0 = kf0, dxn[NX];
 #pragma unroll
-                        for (int j = 0; j < NX; ++j) { du0 += K0[j] * dxmine[j]; du1 += K1[j] * dxmine[j]; }
+                        for (int j = 0; j < NX; ++j) {
+                            const double K1 = -S.Y[k][1][j] * il11;
+                            const double K0 = (-S.Y[k][0][j] - l10 * K1) * il00;
+                            du0 += K0 * dxmine[j];
+                            du1 += K1 * dxmine[j];
+                        }
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            double acc = e[i];
+                            double a = e[i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += G[i][j] * dxmine[j];
-                            dxn[i] = acc;
+                            for (int j = 0; j < NX; ++j) a += G[j][i] * dxmine[j];
+                            dxn[i] = a;
                         }
                         S.ddz[k][0] = du0;
                         S.ddz[k][1] = du1;
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             S.ddz[k][NU + i] = (k == 0) ? 0.0 : dxmine[i];
-                            double acc = pmine[i];
+                            double a = pmine[i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) acc += P1[sym(i, j)] * dxn[j];
-                            S.pin[k][i] = acc;
+                            for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
+                            S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
                             S.ddz[N][0] = 0.0;
@@ -658,87 +696,84 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     }
                 }
                 __syncthreads();
-                // ---- inequality steps and step length (dt, dl recomputed where needed)
-                double amax = 1e300;
-                double ddk[NZ];
+                STAMP_END(5);
+                // ---- inequality steps, step length, predictor statistics, row update
+                STAMP_BEGIN();
+                {
+                    double ddk[NZ];
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) ddk[i] = S.ddz[k < N ? k : N][i];
-                const double smu = sigma_mu;
-                const int ph = phase;
-                auto row_step = [&](auto Pc, int s, double& dt, double& dl) {
-                    constexpr int P = decltype(Pc)::value;
-                    double dot;
-                    if (s < C::nbox(P)) {
-                        dot = box_sign(s) * ddk[box_var(s)];
-                    } else {
-                        const int hh = C::hb(P) + s - C::nbox(P);
-                        dot = S.Dg[k][hh][0] * ddk[2] + S.Dg[k][hh][1] * ddk[3] + S.Dg[k][hh][2] * ddk[4];
-                    }
-                    const double l = R.l[s], t = R.t[s];
-                    const double rc = (ph == 0) ? l * t : l * t + R.pr[s] - smu;
-                    dt = -R.rin[s] - dot;
-                    dl = -(rc + l * dt) / t;
-                };
-                if (k < N) {
-                    on_part<C>(part, [&](auto Pc) {
-                        constexpr int P = decltype(Pc)::value;
+                    for (int i = 0; i < NZ; ++i) ddk[i] = S.ddz[ks][i];
+                    const double smu = sigma_mu;
+                    const int ph = phase;
+                    // dt = -rin - D ddz; dl = -(rc + l dt) / t
+                    auto row_step = [&](auto Cc, int hoff, int s, double& dt, double& dl) {
+                        constexpr int CL = decltype(Cc)::value;
+                        const double l = R.l[s], t = R.t[s];
+                        const double rc = (ph == 0) ? l * t : l * t + R.pr[s] - smu;
+                        dt = -R.rin[s] - row_dot<C, CL>(S.Dg[kc], s, hoff, ddk);
+                        dl = -(rc + l * dt) * R.it[s];
+                    };
+                    // step to the boundary: min over rows of -t/dt and -l/dl = 1 / max(-dt/t, -dl/l)
+                    double rmax = 0.0;
+                    on_class<C>(part, [&](auto Cc, int hoff) {
+                        constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                        for (int s = 0; s < C::nslot(P); ++s) {
-                            if (!row_active<C, P>(s, k)) continue;
+                        for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                            if (!row_active<C, CL>(s, k, hoff)) continue;
                             double dt, dl;
-                            row_step(Pc, s, dt, dl);
-                            if (dt < 0.0) amax = fmin(amax, -R.t[s] / dt);
-                            if (dl < 0.0) amax = fmin(amax, -R.l[s] / dl);
+                            row_step(Cc, hoff, s, dt, dl);
+                            rmax = fmax(rmax, -dt * R.it[s]);
+                            if (dl < 0.0) rmax = fmax(rmax, -dl / R.l[s]);
                         }
                     });
-                }
-                amax = wave_min(amax);
-                if (phase == 0) {
-                    const double aa = fmin(amax, 1.0);
-                    double ca = 0.0;
-                    if (k < N) {
-                        on_part<C>(part, [&](auto Pc) {
-                            constexpr int P = decltype(Pc)::value;
+                    rmax = wave_max(rmax);
+                    const double amax = rmax > 0.0 ? 1.0 / rmax : 1e300;
+                    if (phase == 0) {
+                        const double aa = fmin(amax, 1.0);
+                        double ca = 0.0;
+                        on_class<C>(part, [&](auto Cc, int hoff) {
+                            constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                            for (int s = 0; s < C::nslot(P); ++s) {
-                                if (!row_active<C, P>(s, k)) continue;
+                            for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                                if (!row_active<C, CL>(s, k, hoff)) continue;
                                 double dt, dl;
-                                row_step(Pc, s, dt, dl);
+                                row_step(Cc, hoff, s, dt, dl);
                                 ca += (R.l[s] + aa * dl) * (R.t[s] + aa * dt);
                                 R.pr[s] = dt * dl;
                             }
                         });
-                    }
-                    ca = wave_sum(ca);
-                    const double mu_aff = ca / C::M_TOTAL;
-                    double sig = mu_aff / mu;
-                    if (sig > 1.0) sig = 1.0;
-                    sig = sig * sig * sig;
-                    sigma_mu = sig * mu;
-                } else {
-                    alpha = 0.995 * amax;
-                    if (alpha > 1.0) alpha = 1.0;
-                    if (alpha >= 1e-12 && k < N) {
-                        // row update with the corrector step (before dz moves: rin and
-                        // ddz belong to the current iterate)
-                        on_part<C>(part, [&](auto Pc) {
-                            constexpr int P = decltype(Pc)::value;
+                        ca = wave_sum(ca);
+                        const double mu_aff = ca / C::M_TOTAL;
+                        double sig = mu_aff / mu;
+                        if (sig > 1.0) sig = 1.0;
+                        sig = sig * sig * sig;
+                        sigma_mu = sig * mu;
+                    } else {
+                        alpha = 0.995 * amax;
+                        if (alpha > 1.0) alpha = 1.0;
+                        if (alpha >= 1e-12) {
+                            // rows move with the corrector step (rin, ddz of the current iterate)
+                            on_class<C>(part, [&](auto Cc, int hoff) {
+                                constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                            for (int s = 0; s < C::nslot(P); ++s) {
-                                if (!row_active<C, P>(s, k)) continue;
-                                double dt, dl;
-                                row_step(Pc, s, dt, dl);
-                                R.t[s] += alpha * dt;
-                                R.l[s] += alpha * dl;
-                            }
-                        });
+                                for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
+                                    if (!row_active<C, CL>(s, k, hoff)) continue;
+                                    double dt, dl;
+                                    row_step(Cc, hoff, s, dt, dl);
+                                    R.t[s] += alpha * dt;
+                                    R.l[s] += alpha * dl;
+                                }
+                            });
+                        }
                     }
                 }
                 __syncthreads();
+                STAMP_END(7);
             }
             if (qstat == AC_NAN) break;
             if (alpha < 1e-12) { qstat = AC_MINSTEP; ++qit; break; }
             // ---- update of the stage variables (rows were updated with the step)
+            STAMP_BEGIN();
             if (stage_lane) {
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) S.dz[k][i] += alpha * S.ddz[k][i];
@@ -748,6 +783,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 }
             }
             __syncthreads();
+            STAMP_END(8);
         }
         __syncthreads();
         qp_status = qstat;
@@ -768,10 +804,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             }
         }
         if (k >= 1 && k < N) {
-            on_part<C>(part, [&](auto Pc) {
-                constexpr int P = decltype(Pc)::value;
+            on_class<C>(part, [&](auto Cc, int hoff) {
+                constexpr int CL = decltype(Cc)::value;
+                constexpr int NB = RowClass<C, CL>::NB;
 #pragma unroll
-                for (int s = C::nbox(P); s < C::nslot(P); ++s) R.nlam[s - C::nbox(P)] = R.l[s];
+                for (int s = NB; s < RowClass<C, CL>::NS; ++s) R.nlam[s - NB] = R.l[s];
             });
         }
         __syncthreads();
@@ -806,6 +843,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             info_out[(size_t)sol * MPCG_INFO_STRIDE + 3] = 0;
         }
     }
+    STAMP_STORE(stamps, sol);
 }
 
 }  // namespace mpcg
