@@ -6,7 +6,7 @@
  * independent `MPCPlanner::Solver::solve()` calls inside
  * `GuidanceConstraints::optimize` (mpc_planner_modules/src/guidance_constraints.cpp:304-421)
  * and the acados SQP-RTI solve each of them runs
- * (mpc_planner_solver/src/acados_solver_interface.cpp:311-429).
+ * (mpc_planner_solver/src/acados_solver_interface.cpp:86-119, 162-204).
  *
  * Plain pointers and sizes only.  Buffers use the reference's own layouts:
  *   params  [batch][N][npar]      == AcadosParameters::all_parameters, horizon-major
@@ -17,7 +17,7 @@
  *   utraj   [batch][N][nu]        == AcadosOutput::utraj (:130)
  *   pobj    [batch]               == AcadosInfo::pobj (:108)
  *   exit    [batch]               == return value of Solver::solve(): 1 success, 0 failure,
- *                                    2 max-iter, 3 min-step, 4 QP failure (:423-428)
+ *                                    2 max-iter, 3 min-step, 4 QP failure (acados_solver_interface.cpp:176-201)
  * Batch element b = scene * n_guesses + guess.
  */
 #ifndef MPCG_H
@@ -30,7 +30,7 @@ extern "C" {
 #define MPCG_NX 5
 #define MPCG_NU 2
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 1
+#define MPCG_ABI_VERSION 2
 
 /* Problem description: the generated solver's dimensions + the parameter
  * map (parameter_map.yaml written by solver_generator/generate_solver.py:34-46)
@@ -63,6 +63,59 @@ typedef struct mpcg_problem {
 
 int mpcg_abi_version(void);
 const char *mpcg_last_error(void);
+
+/* Number of nonlinear-constraint rows per stage (n_lin + n_ell). */
+int mpcg_num_h(const mpcg_problem *pr);
+
+/* Size in doubles of one solve's multiplier block: N * (nx + nh). */
+int mpcg_lam_size(const mpcg_problem *pr);
+
+/* Fill `pr` from a parameter map (the name -> index pairs of
+ * parameter_map.yaml) and the solver settings: the module bundles are found
+ * by the names the reference's generator gives them (mpc_base.py, contouring.py,
+ * consistency_module.py, guidance_constraints.py:333-338,
+ * ellipsoid_constraints.py:406-419); n_lin / n_ell / n_seg are counted from
+ * `lin_constraint_<i>_a1`, `ellipsoid_obst_<j>_x`, `spline<i>_start`.
+ * lb/ub: nvar bounds in z order [u x] (model_map.yaml columns 3, 4).
+ * Options take the defaults listed in mpcg_problem.  Returns 0, or -1 with
+ * mpcg_last_error() naming the missing entry. */
+int mpcg_problem_from_map(mpcg_problem *pr, int N, int npar, int n_entries, const char *const *names,
+                          const int *indices, const double *lb, const double *ub, double dt,
+                          int sqp_iters);
+
+/* Input/output buffers of one batched solve (all device pointers for
+ * mpcg_solve, all host pointers for mpcg_context_solve).
+ *   lam_in / lam_out  [batch][N][nx + nh]: NLP multipliers that persist in the
+ *     acados capsule between Solver::solve() calls (ocp_nlp_out pi and lam;
+ *     acados_solver_interface.cpp:86-119, reset to zero by Solver_acados_reset
+ *     on failure, :186-190): per stage k < N the dynamics multipliers pi_k
+ *     (x_{k+1} = phi(z_k)) then, for each h row, the multiplier of its finite
+ *     side (>= 0; stage 0 rows are not part of the QP and stay 0).
+ *     lam_in NULL = zero multipliers (a fresh or reset solver).  lam_out may be
+ *     NULL; on a QP failure it holds the multipliers of the last accepted step. */
+typedef struct mpcg_io {
+    const double *params, *warm, *xinit;
+    const double *lam_in;
+    double *xtraj, *utraj, *pobj;
+    int *exit_code, *info;
+    double *lam_out;
+} mpcg_io;
+
+/* Batched solve on device buffers, enqueued on `stream` (hipStream_t, NULL =
+ * default stream).  Returns 0 on a successful launch. */
+int mpcg_solve(const mpcg_problem *pr, int batch, const mpcg_io *io, void *stream);
+
+/* A persistent solve context: device buffers and pinned staging for up to
+ * `max_batch` solves plus a private stream, so that one Solver::solve()
+ * (batch 1) or one GuidanceConstraints::optimize fan-out (batch = guesses)
+ * costs two copies and one launch.  Not thread-safe per context; contexts are
+ * independent (one per planner thread, like the reference's one capsule per
+ * Solver). */
+typedef struct mpcg_context mpcg_context;
+mpcg_context *mpcg_context_create(const mpcg_problem *pr, int max_batch);
+void mpcg_context_destroy(mpcg_context *ctx);
+/* host pointers; synchronous.  Returns 0, or < 0 with mpcg_last_error(). */
+int mpcg_context_solve(mpcg_context *ctx, int batch, const mpcg_io *io);
 
 /* 0 if (N, n_lin, n_ell) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);

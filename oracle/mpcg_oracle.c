@@ -711,10 +711,18 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters) {
 }
 
 /* ------------------------------------------------------------------ */
-/* Solver::solve() (acados_solver_interface.cpp:311-429)              */
+/* Solver::solve() (acados_solver_interface.cpp:86-119, 162-204)              */
 /* ------------------------------------------------------------------ */
 int orc_solve(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
               double *xtraj, double *utraj, orc_info *info) {
+    return orc_solve_ex(pr, params, warm, xinit, NULL, xtraj, utraj, NULL, info);
+}
+
+/* side of the single finite bound of h row r: 1 upper, 0 lower */
+static int h_side(const double *uh, int r) { return uh[r] < BIGBOUND ? 1 : 0; }
+
+int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
+                 const double *lam_in, double *xtraj, double *utraj, double *lam_out, orc_info *info) {
     int N = pr->N, npar = pr->npar;
     int nh = orc_num_h(pr);
     int maxi = 2 * NZ + 2 * nh;
@@ -737,14 +745,24 @@ int orc_solve(const orc_problem *pr, const double *params, const double *warm, c
         S->dl_aff = dbl + 6 * nrow + o; S->rin = dbl + 7 * nrow + o; S->rc = dbl + 8 * nrow + o;
         S->hrow = ibl + o; S->hsgn = ibl + nrow + o;
     }
-    /* NLP iterate: z_k = [u_k; x_k] from the warm start (loadWarmstart, :499-509);
-     * NLP multipliers start at zero (fresh capsule). */
+    /* NLP iterate: z_k = [u_k; x_k] from the warm start (loadWarmstart, acados_solver_interface.cpp:274-284);
+     * NLP multipliers: those the capsule kept from the previous solve
+     * (lam_in, [N][NX + nh]) or zero (fresh / reset capsule). */
     double (*z)[NZ] = (double (*)[NZ])calloc(N + 1, sizeof(double[NZ]));
     double (*pi)[NX] = (double (*)[NX])calloc(N + 1, sizeof(double[NX]));
     double *lamh = (double *)calloc((size_t)(N + 1) * 2 * nh, sizeof(double)); /* [k][2*i+side] */
     for (int k = 0; k <= N; k++)
         for (int i = 0; i < NZ; i++) z[k][i] = warm[k * NZ + i];
     for (int i = 0; i < NU; i++) z[N][i] = 0.0;
+    const int LS = NX + nh;
+    if (lam_in) {
+        for (int k = 0; k < N; k++) {
+            for (int i = 0; i < NX; i++) pi[k][i] = lam_in[(size_t)k * LS + i];
+            if (k >= 1)
+                for (int r = 0; r < nh; r++)
+                    lamh[(size_t)k * 2 * nh + 2 * r + h_side(uh, r)] = lam_in[(size_t)k * LS + NX + r];
+        }
+    }
 
     double h[ORC_MAX_LIN + ORC_MAX_ELL], jac[(ORC_MAX_LIN + ORC_MAX_ELL) * NZ];
     double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
@@ -824,7 +842,7 @@ int orc_solve(const orc_problem *pr, const double *params, const double *warm, c
                 for (int j = 0; j < NX; j++) S->H[NU + i][NU + j] = Hx[i * NX + j];
             S->ni = 0;
         }
-        /* x0 elimination: lbx_0 = ubx_0 = xinit (:349-350) */
+        /* x0 elimination: lbx_0 = ubx_0 = xinit (acados_solver_interface.cpp:124-125) */
         for (int i = 0; i < NX; i++) w.st[0].dz[NU + i] = xinit[i] - z[0][NU + i];
 
         /* ---- feedback phase: QP ---- */
@@ -847,7 +865,7 @@ int orc_solve(const orc_problem *pr, const double *params, const double *warm, c
         }
         for (int i = 0; i < NU; i++) z[N][i] = 0.0;
         acados_status = AC_SUCCESS;
-        /* acados_solver_interface.cpp:330: break when the QP did not succeed */
+        /* acados_solver_interface.cpp:105: break when the QP did not succeed */
         if (qp_status != AC_SUCCESS) break;
     }
 
@@ -861,6 +879,14 @@ int orc_solve(const orc_problem *pr, const double *params, const double *warm, c
         for (int i = 0; i < NX; i++) xtraj[k * NX + i] = z[k][NU + i];
     for (int k = 0; k < N; k++)
         for (int i = 0; i < NU; i++) utraj[k * NU + i] = z[k][i];
+
+    if (lam_out) {
+        for (int k = 0; k < N; k++) {
+            for (int i = 0; i < NX; i++) lam_out[(size_t)k * LS + i] = pi[k][i];
+            for (int r = 0; r < nh; r++)
+                lam_out[(size_t)k * LS + NX + r] = k >= 1 ? lamh[(size_t)k * 2 * nh + 2 * r + h_side(uh, r)] : 0.0;
+        }
+    }
 
     int exit_code = acados_status;
     if (res_eq > pr->res_eq_fail && exit_code == AC_SUCCESS) exit_code = AC_QP_FAILURE;
@@ -891,6 +917,27 @@ void orc_solve_batch(const orc_problem *pr, int batch, const double *params, con
         status[b] = orc_solve(pr, params + (size_t)b * N * pr->npar, warm + (size_t)b * (N + 1) * NZ,
                               xinit + (size_t)b * NX, xtraj + (size_t)b * (N + 1) * NX,
                               utraj + (size_t)b * N * NU, &info);
+        pobj[b] = info.pobj;
+        if (qp_iters) qp_iters[b] = info.qp_iter_total;
+    }
+    (void)nthreads;
+}
+
+void orc_solve_batch_ex(const orc_problem *pr, int batch, const double *params, const double *warm,
+                        const double *xinit, const double *lam_in, double *xtraj, double *utraj, double *pobj,
+                        int *status, int *qp_iters, double *lam_out, int nthreads) {
+    int N = pr->N;
+    size_t LS = (size_t)N * (NX + orc_num_h(pr));
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+#endif
+    for (int b = 0; b < batch; b++) {
+        orc_info info;
+        status[b] = orc_solve_ex(pr, params + (size_t)b * N * pr->npar, warm + (size_t)b * (N + 1) * NZ,
+                                 xinit + (size_t)b * NX, lam_in ? lam_in + b * LS : NULL,
+                                 xtraj + (size_t)b * (N + 1) * NX, utraj + (size_t)b * N * NU,
+                                 lam_out ? lam_out + b * LS : NULL, &info);
         pobj[b] = info.pobj;
         if (qp_iters) qp_iters[b] = info.qp_iter_total;
     }

@@ -71,6 +71,8 @@ def lib():
         L.orc_solve.argtypes = [P, dp, dp, dp, dp, dp, C.POINTER(OrcInfo)]
         L.orc_solve.restype = C.c_int
         L.orc_solve_batch.argtypes = [P, C.c_int, dp, dp, dp, dp, dp, dp, ip, ip, C.c_int]
+        vp = C.c_void_p
+        L.orc_solve_batch_ex.argtypes = [P, C.c_int, dp, dp, dp, vp, dp, dp, dp, ip, ip, vp, C.c_int]
         _lib = L
     return _lib
 
@@ -167,9 +169,25 @@ class Oracle:
                     sqp_iter=info.sqp_iter, qp_iter=info.qp_iter_total, qp_status=info.qp_status,
                     res_eq=info.res_eq)
 
-    def solve_batch(self, params, warm, xinit, nthreads=0):
+    def lam_size(self):
+        return self.layout.N * (5 + self.layout.nh)
+
+    def solve_batch(self, params, warm, xinit, nthreads=0, lam_in=None, return_lam=False):
+        """lam_in / returned lam: [B, N, 5 + nh] NLP multipliers (include/mpcg.h, mpcg_io)."""
         N = self.layout.N
         B = params.shape[0]
+        if lam_in is not None or return_lam:
+            xt, ut = np.zeros((B, N + 1, 5)), np.zeros((B, N, 2))
+            pobj, st, qi = np.zeros(B), np.zeros(B, np.int32), np.zeros(B, np.int32)
+            li = None if lam_in is None else np.ascontiguousarray(lam_in, float).reshape(B, -1)
+            lo = np.zeros((B, N, 5 + self.layout.nh))
+            self.L.orc_solve_batch_ex(C.byref(self.pr), B, np.ascontiguousarray(params, float).reshape(-1),
+                                      np.ascontiguousarray(warm, float).reshape(-1),
+                                      np.ascontiguousarray(xinit, float).reshape(-1),
+                                      None if li is None else li.ctypes.data_as(C.c_void_p),
+                                      xt.reshape(-1), ut.reshape(-1), pobj, st, qi,
+                                      lo.ctypes.data_as(C.c_void_p), nthreads)
+            return dict(xtraj=xt, utraj=ut, pobj=pobj, status=st, qp_iter=qi, lam=lo)
         xt = np.zeros((B, N + 1, 5))
         ut = np.zeros((B, N, 2))
         pobj = np.zeros(B)

@@ -3,7 +3,7 @@
 // One wavefront (64 lanes, one workgroup) solves one (scene, guess) pair:
 // the body of one `Solver::solve()` call of the OpenMP fan-out in
 // GuidanceConstraints::optimize (guidance_constraints.cpp:304-421), i.e.
-// `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:311-429).
+// `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:86-119).
 //
 // Lane roles inside the wave
 //   * stage lanes   lane k in [0, N]: linearisation of shooting stage k (cost,
@@ -70,11 +70,8 @@ static thread_local std::string g_err;
 static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG_STAMPS builds only)
 
 template <class C>
-static int launch(const mpcg_problem& pr, int batch, const double* params, const double* warm,
-                  const double* xinit, double* xtraj, double* utraj, double* pobj, int* exit_code,
-                  int* info, hipStream_t stream) {
-    hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, stream, pr, batch, params, warm, xinit,
-                       xtraj, utraj, pobj, exit_code, info, g_stamps);
+static int launch(const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream) {
+    hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, stream, pr, batch, io, g_stamps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("sqp_kernel launch: ") + hipGetErrorString(e);
@@ -83,8 +80,7 @@ static int launch(const mpcg_problem& pr, int batch, const double* params, const
     return 0;
 }
 
-using Fn = int (*)(const mpcg_problem&, int, const double*, const double*, const double*, double*, double*,
-                   double*, int*, int*, hipStream_t);
+using Fn = int (*)(const mpcg_problem&, int, const mpcg_io&, hipStream_t);
 
 static Fn find_instance(const mpcg_problem& pr) {
     if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return nullptr;
@@ -98,72 +94,235 @@ static Fn find_instance(const mpcg_problem& pr) {
     return nullptr;
 }
 
+static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
+    if (!pr || batch < 0) { g_err = "invalid arguments"; return -1; }
+    *fn = find_instance(*pr);
+    if (!*fn) {
+        g_err = "no compiled instance for N=" + std::to_string(pr->N) + " n_lin=" + std::to_string(pr->n_lin) +
+                " n_ell=" + std::to_string(pr->n_ell);
+        return -2;
+    }
+    return 0;
+}
+
 }  // namespace mpcg
+
+// Persistent context (include/mpcg.h): one device allocation for every
+// buffer of `max_batch` solves, one pinned staging block, a private stream.
+struct mpcg_context {
+    mpcg_problem pr;
+    int max_batch = 0;
+    hipStream_t stream = nullptr;
+    double* dev = nullptr;   // params | warm | xinit | lam_in | xtraj | utraj | pobj | lam_out
+    double* host = nullptr;  // pinned mirror of the same layout
+    int* idev = nullptr;     // exit | info
+    int* ihost = nullptr;
+    size_t n_par, n_warm, n_xi, n_lam, n_xt, n_ut, n_dbl, n_int;
+};
 
 extern "C" {
 
 int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
 
-/* diagnostic builds only: device buffer of batch x 10 u64 phase-cycle sums */
+/* diagnostic builds only: device buffer of batch x 16 u64 phase-cycle sums */
 void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps = dev_ptr; }
 
 const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }
 
 int mpcg_supported(const mpcg_problem* pr) { return (pr && mpcg::find_instance(*pr)) ? 0 : -1; }
 
+int mpcg_num_h(const mpcg_problem* pr) { return pr ? pr->n_lin + pr->n_ell : 0; }
+
+int mpcg_lam_size(const mpcg_problem* pr) { return pr ? pr->N * (MPCG_NX + mpcg_num_h(pr)) : 0; }
+
+int mpcg_problem_from_map(mpcg_problem* pr, int N, int npar, int n_entries, const char* const* names,
+                          const int* indices, const double* lb, const double* ub, double dt, int sqp_iters) {
+    if (!pr || !names || !indices || !lb || !ub || N < 1 || npar < 1 || n_entries < 0) {
+        mpcg::g_err = "invalid arguments";
+        return -1;
+    }
+    auto find = [&](const std::string& nm) {
+        for (int i = 0; i < n_entries; ++i)
+            if (names[i] && nm == names[i]) return indices[i];
+        return -1;
+    };
+    std::memset(pr, 0, sizeof(*pr));
+    pr->N = N;
+    pr->npar = npar;
+    // MPCBase weights (mpc_base.py:47-60), contouring (contouring.py:114-138)
+    pr->i_w_acc = find("acceleration");
+    pr->i_w_ang = find("angular_velocity");
+    pr->i_w_vel = find("velocity");
+    pr->i_v_ref = find("reference_velocity");
+    pr->i_w_contour = find("contour");
+    pr->i_w_lag = find("lag");
+    pr->i_spline0 = find("spline_x0_a");
+    // consistency (consistency_module.py:220-227): optional
+    pr->i_cons_w = find("consistency_weight");
+    pr->i_prev_x = find("prev_traj_x");
+    pr->i_prev_y = find("prev_traj_y");
+    // disc + obstacles (ellipsoid_constraints.py:406-419), topology halfspaces (guidance_constraints.py:333-338)
+    pr->i_disc_r = find("ego_disc_radius");
+    pr->i_disc_off = find("ego_disc_0_offset");
+    pr->i_lin0 = find("lin_constraint_0_a1");
+    pr->i_ell0 = find("ellipsoid_obst_0_x");
+    const char* required[] = {"acceleration", "angular_velocity", "velocity", "reference_velocity", "contour",
+                              "lag", "spline_x0_a", "ego_disc_radius", "ego_disc_0_offset"};
+    for (const char* r : required)
+        if (find(r) < 0) { mpcg::g_err = std::string("parameter map has no '") + r + "'"; return -1; }
+    while (find("spline" + std::to_string(pr->n_seg) + "_start") >= 0) ++pr->n_seg;
+    while (find("lin_constraint_" + std::to_string(pr->n_lin) + "_a1") >= 0) ++pr->n_lin;
+    while (find("ellipsoid_obst_" + std::to_string(pr->n_ell) + "_x") >= 0) ++pr->n_ell;
+    // the kernels read bundles at fixed strides from their base index: check them
+    for (int j = 0; j < pr->n_seg; ++j)
+        if (find("spline_y" + std::to_string(j) + "_d") != pr->i_spline0 + 9 * j + 7 ||
+            find("spline" + std::to_string(j) + "_start") != pr->i_spline0 + 9 * j + 8) {
+            mpcg::g_err = "spline segment " + std::to_string(j) + " is not contiguous";
+            return -1;
+        }
+    for (int i = 0; i < pr->n_lin; ++i)
+        if (find("lin_constraint_" + std::to_string(i) + "_b") != pr->i_lin0 + 3 * i + 2) {
+            mpcg::g_err = "halfspace " + std::to_string(i) + " is not contiguous";
+            return -1;
+        }
+    for (int j = 0; j < pr->n_ell; ++j)
+        if (find("ellipsoid_obst_" + std::to_string(j) + "_r") != pr->i_ell0 + 7 * j + 6) {
+            mpcg::g_err = "obstacle " + std::to_string(j) + " is not contiguous";
+            return -1;
+        }
+    pr->dt = dt;
+    pr->rk_steps = 3;  // sim_method_num_steps (generate_acados_solver.py:148-150)
+    for (int i = 0; i < MPCG_NU; ++i) { pr->lbu[i] = lb[i]; pr->ubu[i] = ub[i]; }
+    for (int i = 0; i < MPCG_NX; ++i) { pr->lbx[i] = lb[MPCG_NU + i]; pr->ubx[i] = ub[MPCG_NU + i]; }
+    pr->sqp_iters = sqp_iters;
+    pr->qp_tol = 1e-5;
+    pr->qp_iter_max = 50;
+    pr->reg_eps = 1e-4;
+    pr->qp_mu0 = 1.0;
+    pr->qp_thr0 = 1.0;
+    pr->res_eq_fail = 1e-2;
+    return 0;
+}
+
+int mpcg_solve(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream) {
+    mpcg::Fn fn;
+    int rc = mpcg::check_problem(pr, batch, &fn);
+    if (rc) return rc;
+    if (!io || !io->params || !io->warm || !io->xinit || !io->xtraj || !io->utraj || !io->pobj || !io->exit_code) {
+        mpcg::g_err = "missing buffer";
+        return -1;
+    }
+    if (batch == 0) return 0;
+    return fn(*pr, batch, *io, (hipStream_t)stream);
+}
+
 int mpcg_solve_batch_device(const mpcg_problem* pr, int batch, const double* params, const double* warm,
                             const double* xinit, double* xtraj, double* utraj, double* pobj, int* exit_code,
                             int* info, void* stream) {
-    if (!pr || batch < 0) { mpcg::g_err = "invalid arguments"; return -1; }
-    if (batch == 0) return 0;
-    mpcg::Fn fn = mpcg::find_instance(*pr);
-    if (!fn) {
-        mpcg::g_err = "no compiled instance for N=" + std::to_string(pr->N) + " n_lin=" + std::to_string(pr->n_lin) +
-                      " n_ell=" + std::to_string(pr->n_ell);
-        return -2;
+    mpcg_io io{params, warm, xinit, nullptr, xtraj, utraj, pobj, exit_code, info, nullptr};
+    return mpcg_solve(pr, batch, &io, stream);
+}
+
+mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
+    mpcg::Fn fn;
+    if (mpcg::check_problem(pr, max_batch, &fn)) return nullptr;
+    if (max_batch < 1) { mpcg::g_err = "max_batch must be >= 1"; return nullptr; }
+    auto* c = new mpcg_context();
+    c->pr = *pr;
+    c->max_batch = max_batch;
+    const size_t B = max_batch, N = pr->N;
+    c->n_par = B * N * pr->npar;
+    c->n_warm = B * (N + 1) * MPCG_NVAR;
+    c->n_xi = B * MPCG_NX;
+    c->n_lam = B * (size_t)mpcg_lam_size(pr);
+    c->n_xt = B * (N + 1) * MPCG_NX;
+    c->n_ut = B * N * MPCG_NU;
+    c->n_dbl = c->n_par + c->n_warm + c->n_xi + 2 * c->n_lam + c->n_xt + c->n_ut + B;
+    c->n_int = B * (1 + MPCG_INFO_STRIDE);
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&c->dev, c->n_dbl * sizeof(double)) == hipSuccess &&
+              hipHostMalloc(&c->host, c->n_dbl * sizeof(double), hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&c->idev, c->n_int * sizeof(int)) == hipSuccess &&
+              hipHostMalloc(&c->ihost, c->n_int * sizeof(int), hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
+        mpcg::g_err = "mpcg_context_create: device allocation failed";
+        mpcg_context_destroy(c);
+        return nullptr;
     }
-    return fn(*pr, batch, params, warm, xinit, xtraj, utraj, pobj, exit_code, info, (hipStream_t)stream);
+    return c;
+}
+
+void mpcg_context_destroy(mpcg_context* c) {
+    if (!c) return;
+    if (c->dev) (void)hipFree(c->dev);
+    if (c->idev) (void)hipFree(c->idev);
+    if (c->host) (void)hipHostFree(c->host);
+    if (c->ihost) (void)hipHostFree(c->ihost);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
+    if (!c || !io || batch < 0 || batch > c->max_batch) {
+        mpcg::g_err = "mpcg_context_solve: invalid arguments or batch > max_batch";
+        return -1;
+    }
+    if (!io->params || !io->warm || !io->xinit || !io->xtraj || !io->utraj || !io->pobj || !io->exit_code) {
+        mpcg::g_err = "missing buffer";
+        return -1;
+    }
+    if (batch == 0) return 0;
+    const mpcg_problem& pr = c->pr;
+    const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr);
+    const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * MPCG_NVAR, s_xi = B * MPCG_NX, s_lam = B * L;
+    const size_t s_xt = B * (N + 1) * MPCG_NX, s_ut = B * N * MPCG_NU;
+    // inputs are packed contiguously (params | warm | xinit | lam_in) so one copy moves them
+    double* h = c->host;
+    std::memcpy(h, io->params, s_par * sizeof(double));
+    std::memcpy(h + s_par, io->warm, s_warm * sizeof(double));
+    std::memcpy(h + s_par + s_warm, io->xinit, s_xi * sizeof(double));
+    size_t n_in = s_par + s_warm + s_xi;
+    if (io->lam_in) {
+        std::memcpy(h + n_in, io->lam_in, s_lam * sizeof(double));
+        n_in += s_lam;
+    }
+    double* d = c->dev;
+    double* d_out = d + c->n_par + c->n_warm + c->n_xi + c->n_lam;  // xtraj | utraj | pobj | lam_out
+    mpcg_io dio{d, d + s_par, d + s_par + s_warm, io->lam_in ? d + s_par + s_warm + s_xi : nullptr,
+                d_out, d_out + s_xt, d_out + s_xt + s_ut, c->idev, c->idev + B,
+                io->lam_out ? d_out + s_xt + s_ut + B : nullptr};
+    const size_t n_out = s_xt + s_ut + B + (io->lam_out ? s_lam : 0);
+    double* h_out = c->host + c->n_par + c->n_warm + c->n_xi + c->n_lam;
+    bool ok = hipMemcpyAsync(d, h, n_in * sizeof(double), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    int rc = ok ? mpcg_solve(&pr, batch, &dio, c->stream) : -5;
+    if (rc == 0)
+        ok = hipMemcpyAsync(h_out, d_out, n_out * sizeof(double), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+             hipMemcpyAsync(c->ihost, c->idev, B * (1 + MPCG_INFO_STRIDE) * sizeof(int), hipMemcpyDeviceToHost,
+                            c->stream) == hipSuccess;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (!ok || e != hipSuccess) {
+        mpcg::g_err = std::string("mpcg_context_solve: ") + hipGetErrorString(e != hipSuccess ? e : hipGetLastError());
+        return rc ? rc : -4;
+    }
+    if (rc) return rc;
+    std::memcpy(io->xtraj, h_out, s_xt * sizeof(double));
+    std::memcpy(io->utraj, h_out + s_xt, s_ut * sizeof(double));
+    std::memcpy(io->pobj, h_out + s_xt + s_ut, B * sizeof(double));
+    if (io->lam_out) std::memcpy(io->lam_out, h_out + s_xt + s_ut + B, s_lam * sizeof(double));
+    std::memcpy(io->exit_code, c->ihost, B * sizeof(int));
+    if (io->info) std::memcpy(io->info, c->ihost + B, B * MPCG_INFO_STRIDE * sizeof(int));
+    return 0;
 }
 
 int mpcg_solve_batch_host(const mpcg_problem* pr, int batch, const double* params, const double* warm,
                           const double* xinit, double* xtraj, double* utraj, double* pobj, int* exit_code,
                           int* info) {
-    if (!pr || batch < 0) { mpcg::g_err = "invalid arguments"; return -1; }
-    if (batch == 0) return 0;
-    const size_t N = pr->N, np = pr->npar;
-    const size_t s_par = batch * N * np, s_warm = batch * (N + 1) * MPCG_NVAR, s_xi = (size_t)batch * MPCG_NX;
-    const size_t s_xt = batch * (N + 1) * MPCG_NX, s_ut = batch * N * MPCG_NU;
-    double *dpar, *dwarm, *dxi, *dxt, *dut, *dpo;
-    int *dex, *dinfo;
-    size_t dbl = s_par + s_warm + s_xi + s_xt + s_ut + batch;
-    if (hipMalloc(&dpar, dbl * sizeof(double)) != hipSuccess) { mpcg::g_err = "hipMalloc failed"; return -3; }
-    if (hipMalloc(&dex, (size_t)batch * (1 + MPCG_INFO_STRIDE) * sizeof(int)) != hipSuccess) {
-        (void)hipFree(dpar);
-        mpcg::g_err = "hipMalloc failed";
-        return -3;
-    }
-    dwarm = dpar + s_par; dxi = dwarm + s_warm; dxt = dxi + s_xi; dut = dxt + s_xt; dpo = dut + s_ut;
-    dinfo = dex + batch;
-    bool ok = hipMemcpy(dpar, params, s_par * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dwarm, warm, s_warm * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dxi, xinit, s_xi * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
-    int rc = ok ? mpcg_solve_batch_device(pr, batch, dpar, dwarm, dxi, dxt, dut, dpo, dex, dinfo, nullptr) : -5;
-    if (!ok) mpcg::g_err = "host to device copy failed";
-    if (rc == 0) {
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) { mpcg::g_err = std::string("solve: ") + hipGetErrorString(e); rc = -4; }
-    }
-    if (rc == 0) {
-        ok = hipMemcpy(xtraj, dxt, s_xt * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(utraj, dut, s_ut * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(pobj, dpo, batch * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(exit_code, dex, batch * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
-             (!info || hipMemcpy(info, dinfo, (size_t)batch * MPCG_INFO_STRIDE * sizeof(int),
-                                 hipMemcpyDeviceToHost) == hipSuccess);
-        if (!ok) { mpcg::g_err = "device to host copy failed"; rc = -5; }
-    }
-    (void)hipFree(dpar);
-    (void)hipFree(dex);
+    if (batch == 0) return pr ? 0 : -1;
+    mpcg_context* c = mpcg_context_create(pr, batch);
+    if (!c) return -3;
+    mpcg_io io{params, warm, xinit, nullptr, xtraj, utraj, pobj, exit_code, info, nullptr};
+    int rc = mpcg_context_solve(c, batch, &io);
+    mpcg_context_destroy(c);
     return rc;
 }
 

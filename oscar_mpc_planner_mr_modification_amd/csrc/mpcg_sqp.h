@@ -2,7 +2,7 @@
 //
 // Reference: one `Solver::solve()` of the OpenMP fan-out in
 // GuidanceConstraints::optimize (guidance_constraints.cpp:304-421) =
-// `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:311-429).
+// `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:86-119).
 //
 // Lane layout (PARTS lanes per shooting stage, lane = k * PARTS + part):
 //   part 0 of stage k  cost / ERK4 / MIRROR / stage algebra of stage k and the
@@ -84,15 +84,19 @@ struct Lds {
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
 // production build compiles them out).  Read shares, not absolute times.
 #ifdef MPCG_STAMPS
-#define STAMP_DECL unsigned long long st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0_ = 0;
-#define STAMP_BEGIN() do { __syncthreads(); st_t0_ = __builtin_amdgcn_s_memtime(); } while (0)
+#define MPCG_NSTAMP 16
+#define STAMP_DECL unsigned long long st_acc_[MPCG_NSTAMP] = {}, st_t0_ = 0, st_l_ = 0;
+#define STAMP_BEGIN() do { __syncthreads(); st_t0_ = __builtin_amdgcn_s_memtime(); st_l_ = st_t0_; } while (0)
 #define STAMP_END(i) do { __syncthreads(); st_acc_[i] += __builtin_amdgcn_s_memtime() - st_t0_; } while (0)
+// sub-phase lap inside a phase (the wave runs divergent branches one after the other)
+#define STAMP_LAP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc_[i] += t_ - st_l_; st_l_ = t_; } while (0)
 #define STAMP_STORE(ptr, sol) \
-    do { if ((ptr) && threadIdx.x == 0) for (int i_ = 0; i_ < 10; ++i_) (ptr)[(size_t)(sol) * 10 + i_] = st_acc_[i_]; } while (0)
+    do { if ((ptr) && threadIdx.x == 0) for (int i_ = 0; i_ < MPCG_NSTAMP; ++i_) (ptr)[(size_t)(sol) * MPCG_NSTAMP + i_] = st_acc_[i_]; } while (0)
 #else
 #define STAMP_DECL
 #define STAMP_BEGIN() do {} while (0)
 #define STAMP_END(i) do {} while (0)
+#define STAMP_LAP(i) do {} while (0)
 #define STAMP_STORE(ptr, sol) do {} while (0)
 #endif
 
@@ -230,11 +234,8 @@ __device__ __forceinline__ double row_gap(const mpcg_problem& pr, const double* 
 }
 
 template <class C>
-__global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, const double* __restrict__ params,
-                                                    const double* __restrict__ warm, const double* __restrict__ xinit,
-                                                    double* __restrict__ xtraj, double* __restrict__ utraj,
-                                                    double* __restrict__ pobj_out, int* __restrict__ exit_out,
-                                                    int* __restrict__ info_out, unsigned long long* __restrict__ stamps) {
+__global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
+                                                    unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, PARTS = C::PARTS;
     __shared__ Lds<C> S;
     const int sol = blockIdx.x;
@@ -246,20 +247,33 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     const int ks = k <= N ? k : N;       // clamped stage (always a valid LDS index)
     const int kc = k < N ? k : N - 1;    // clamped stage < N
     const int npar = pr.npar;
-    const double* pbase = params + (size_t)sol * N * npar;
+    constexpr int LAMS = NX + C::NH;  // multiplier block per stage (include/mpcg.h, mpcg_io)
+    const double* pbase = io.params + (size_t)sol * N * npar;
     const double* pk = pbase + (size_t)kc * npar;
     (void)stamps;
     STAMP_DECL
 
+    // NLP multipliers carried over from the previous solve of this planner
+    // (zero for a fresh or reset acados capsule)
+    const double* lam_in = io.lam_in ? io.lam_in + (size_t)sol * N * LAMS : nullptr;
     Rows<C> R;
 #pragma unroll
     for (int s = 0; s < C::HSLOTS; ++s) R.nlam[s] = 0.0;
+    if (lam_in && k >= 1 && k < N) {
+        on_class<C>(part, [&](auto Cc, int hoff) {
+            constexpr int CL = decltype(Cc)::value;
+#pragma unroll
+            for (int r = 0; r < RowClass<C, CL>::NHR; ++r)
+                if (hoff + r < C::NH) R.nlam[r] = lam_in[(size_t)k * LAMS + NX + hoff + r];
+        });
+    }
 
-    // ---- load warm start (loadWarmstart, acados_solver_interface.cpp:499-509)
-    const double* w = warm + (size_t)sol * (N + 1) * NZ;
+    // ---- load warm start (loadWarmstart, acados_solver_interface.cpp:274-284)
+    const double* w = io.warm + (size_t)sol * (N + 1) * NZ;
     for (int e = lane; e < (N + 1) * NZ; e += 64) (&S.z[0][0])[e] = w[e];
-    if (lane < NX) S.xinit[lane] = xinit[(size_t)sol * NX + lane];
-    for (int e = lane; e < N * NX; e += 64) (&S.pi_nlp[0][0])[e] = 0.0;
+    if (lane < NX) S.xinit[lane] = io.xinit[(size_t)sol * NX + lane];
+    for (int e = lane; e < N * NX; e += 64)
+        (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
     __syncthreads();
     if (lane < NU) S.z[N][lane] = 0.0;
     __syncthreads();
@@ -282,6 +296,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         h_rows<C, CL>(pr, pk, zk, hoff, R.nlam, hb6, S.Dg[k], S.hd[k]);
                 });
             }
+            STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {
                 double acc[6];
@@ -298,9 +313,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (stage_lane && k < N) {
                 double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
                 stage_cost(pr, pk, zk, g, H, true);
+                STAMP_LAP(11);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
                 erk_unicycle(pr, zk, pi, xn, F, H);
+                STAMP_LAP(12);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     const double bi = xn[i] - S.z[k + 1][NU + i];
@@ -315,7 +332,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 H[2][4] += hb6[2]; H[4][2] += hb6[2];
                 H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
                 H[4][4] += hb6[5];
+                STAMP_LAP(13);
                 mirror7(H, pr.reg_eps);
+                STAMP_LAP(14);
 #pragma unroll
                 for (int i = 0; i < NZ; ++i)
 #pragma unroll
@@ -816,7 +835,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         if (qstat != AC_SUCCESS) break;
     }
 
-    // ---- completeOneIteration (acados_solver_interface.cpp:387-429)
+    // ---- completeOneIteration (acados_solver_interface.cpp:162-204)
     double Lk = 0.0;
     if (stage_lane && k < N) {
         double zz[NZ], gd[NZ], Hd[NZ][NZ];
@@ -825,22 +844,36 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         Lk = stage_cost(pr, pk, zz, gd, Hd, false);
     }
     const double pobj = wave_sum(Lk);
-    double* xo = xtraj + (size_t)sol * (N + 1) * NX;
+    double* xo = io.xtraj + (size_t)sol * (N + 1) * NX;
     for (int e = lane; e < (N + 1) * NX; e += 64) xo[e] = S.z[e / NX][NU + e % NX];
-    double* uo = utraj + (size_t)sol * N * NU;
+    double* uo = io.utraj + (size_t)sol * N * NU;
     for (int e = lane; e < N * NU; e += 64) uo[e] = S.z[e / NU][e % NU];
+    if (io.lam_out) {
+        double* lo = io.lam_out + (size_t)sol * N * LAMS;
+        for (int e = lane; e < N * NX; e += 64) lo[(size_t)(e / NX) * LAMS + e % NX] = S.pi_nlp[e / NX][e % NX];
+        if (k == 0) {
+            for (int r = part; r < C::NH; r += PARTS) lo[NX + r] = 0.0;
+        } else if (k < N) {
+            on_class<C>(part, [&](auto Cc, int hoff) {
+                constexpr int CL = decltype(Cc)::value;
+#pragma unroll
+                for (int r = 0; r < RowClass<C, CL>::NHR; ++r)
+                    if (hoff + r < C::NH) lo[(size_t)k * LAMS + NX + hoff + r] = R.nlam[r];
+            });
+        }
+    }
     if (lane == 0) {
         int code = acados_status;
         if (res_eq > pr.res_eq_fail && code == AC_SUCCESS) code = AC_QP_FAILURE;
         if (code == AC_SUCCESS) code = 1;
         else if (code == 1) code = 0;
-        exit_out[sol] = code;
-        pobj_out[sol] = pobj;
-        if (info_out) {
-            info_out[(size_t)sol * MPCG_INFO_STRIDE + 0] = sqp_iter;
-            info_out[(size_t)sol * MPCG_INFO_STRIDE + 1] = qp_total;
-            info_out[(size_t)sol * MPCG_INFO_STRIDE + 2] = qp_status;
-            info_out[(size_t)sol * MPCG_INFO_STRIDE + 3] = 0;
+        io.exit_code[sol] = code;
+        io.pobj[sol] = pobj;
+        if (io.info) {
+            io.info[(size_t)sol * MPCG_INFO_STRIDE + 0] = sqp_iter;
+            io.info[(size_t)sol * MPCG_INFO_STRIDE + 1] = qp_total;
+            io.info[(size_t)sol * MPCG_INFO_STRIDE + 2] = qp_status;
+            io.info[(size_t)sol * MPCG_INFO_STRIDE + 3] = 0;
         }
     }
     STAMP_STORE(stamps, sol);

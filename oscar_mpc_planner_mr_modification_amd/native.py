@@ -10,8 +10,8 @@ import os
 
 import numpy as np
 
-from .native_spec import (DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX, UNICYCLE_LB,  # noqa: F401
-                          UNICYCLE_UB, MpcgProblem, problem_from_layout)
+from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX,  # noqa: F401
+                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, problem_from_layout)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 # MPCG_LIB selects a diagnostic build (e.g. libmpcg_stamps.so); default the production library
@@ -34,6 +34,17 @@ def _load():
     lib.mpcg_last_error.restype = C.c_char_p
     lib.mpcg_supported.argtypes = [P]
     lib.mpcg_supported.restype = C.c_int
+    lib.mpcg_num_h.argtypes = [P]
+    lib.mpcg_lam_size.argtypes = [P]
+    lib.mpcg_problem_from_map.argtypes = [P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_char_p),
+                                          C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                          C.c_double, C.c_int]
+    lib.mpcg_solve.argtypes = [P, C.c_int, C.POINTER(MpcgIo), vp]
+    lib.mpcg_solve.restype = C.c_int
+    lib.mpcg_context_create.argtypes = [P, C.c_int]
+    lib.mpcg_context_create.restype = vp
+    lib.mpcg_context_destroy.argtypes = [vp]
+    lib.mpcg_context_solve.argtypes = [vp, C.c_int, C.POINTER(MpcgIo)]
     lib.mpcg_solve_batch_device.argtypes = [P, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcg_solve_batch_device.restype = C.c_int
     lib.mpcg_solve_batch_host.argtypes = [P, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -41,6 +52,8 @@ def _load():
     lib.mpcg_select_best_device.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, C.c_double, vp, vp,
                                             C.c_double, vp, vp, vp, vp]
     lib.mpcg_select_best_device.restype = C.c_int
+    if lib.mpcg_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
 
 
@@ -60,18 +73,24 @@ def _check(rc, what):
         raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
 
 
-def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=None):
+def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=None, lam_in=None,
+                       lam_out=False):
     """Batched solve on device tensors (torch, float64, on the current HIP device).
-    params (B, N, npar), warm (B, N+1, 7), xinit (B, 5).  Returns a dict of
-    device tensors; asynchronous on `stream` (torch.cuda stream or None = current)."""
+    params (B, N, npar), warm (B, N+1, 7), xinit (B, 5), optional lam_in
+    (B, N, 5 + nh) NLP multipliers carried over from the previous solve.
+    Returns a dict of device tensors (+ "lam" if lam_out); asynchronous on
+    `stream` (torch.cuda stream or None = current)."""
     import torch
 
     B = params.shape[0]
     N = pr.N
+    LS = NX + pr.n_lin + pr.n_ell
     assert params.dtype == torch.float64 and params.is_cuda and params.is_contiguous()
     assert tuple(params.shape) == (B, N, pr.npar), (tuple(params.shape), (B, N, pr.npar))
     assert tuple(warm.shape) == (B, N + 1, NVAR) and warm.is_contiguous() and warm.dtype == torch.float64
     assert tuple(xinit.shape) == (B, NX) and xinit.is_contiguous() and xinit.dtype == torch.float64
+    if lam_in is not None:
+        assert tuple(lam_in.shape) == (B, N, LS) and lam_in.is_contiguous() and lam_in.dtype == torch.float64
     dev = params.device
     if out is None:
         out = dict(xtraj=torch.empty((B, N + 1, NX), dtype=torch.float64, device=dev),
@@ -79,12 +98,61 @@ def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=No
                    pobj=torch.empty((B,), dtype=torch.float64, device=dev),
                    exit=torch.empty((B,), dtype=torch.int32, device=dev),
                    info=torch.empty((B, INFO_STRIDE), dtype=torch.int32, device=dev))
+    if lam_out and "lam" not in out:
+        out["lam"] = torch.empty((B, N, LS), dtype=torch.float64, device=dev)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
-    rc = lib.mpcg_solve_batch_device(C.byref(pr), B, _ptr(params), _ptr(warm), _ptr(xinit), _ptr(out["xtraj"]),
-                                     _ptr(out["utraj"]), _ptr(out["pobj"]), _ptr(out["exit"]), _ptr(out["info"]),
-                                     C.c_void_p(s.cuda_stream))
-    _check(rc, "mpcg_solve_batch_device")
+    io = MpcgIo(params.data_ptr(), warm.data_ptr(), xinit.data_ptr(),
+                None if lam_in is None else lam_in.data_ptr(),
+                out["xtraj"].data_ptr(), out["utraj"].data_ptr(), out["pobj"].data_ptr(), out["exit"].data_ptr(),
+                out["info"].data_ptr() if out.get("info") is not None else None,
+                out["lam"].data_ptr() if lam_out else None)
+    rc = lib.mpcg_solve(C.byref(pr), B, C.byref(io), C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_solve")
     return out
+
+
+class Context:
+    """A persistent host-buffer solve context (mpcg_context_*): what one
+    drop-in `MPCPlanner::Solver` holds.  Synchronous `solve`."""
+
+    def __init__(self, pr: MpcgProblem, max_batch: int):
+        self.pr = pr
+        self.max_batch = max_batch
+        self._c = lib.mpcg_context_create(C.byref(pr), max_batch)
+        if not self._c:
+            raise RuntimeError(f"mpcg_context_create failed: {last_error()}")
+
+    def close(self):
+        if self._c:
+            lib.mpcg_context_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, params, warm, xinit, lam_in=None, lam_out=False):
+        pr = self.pr
+        B, N = params.shape[0], pr.N
+        LS = NX + pr.n_lin + pr.n_ell
+        params = np.ascontiguousarray(params, np.float64)
+        warm = np.ascontiguousarray(warm, np.float64)
+        xinit = np.ascontiguousarray(xinit, np.float64)
+        assert params.shape == (B, N, pr.npar) and warm.shape == (B, N + 1, NVAR) and xinit.shape == (B, NX)
+        r = dict(xtraj=np.zeros((B, N + 1, NX)), utraj=np.zeros((B, N, NU)), pobj=np.zeros(B),
+                 exit=np.zeros(B, np.int32), info=np.zeros((B, INFO_STRIDE), np.int32))
+        if lam_in is not None:
+            lam_in = np.ascontiguousarray(lam_in, np.float64)
+            assert lam_in.shape == (B, N, LS)
+        if lam_out:
+            r["lam"] = np.zeros((B, N, LS))
+        a = lambda x: None if x is None else x.ctypes.data  # noqa: E731
+        io = MpcgIo(a(params), a(warm), a(xinit), a(lam_in), a(r["xtraj"]), a(r["utraj"]), a(r["pobj"]),
+                    a(r["exit"]), a(r["info"]), a(r.get("lam")))
+        _check(lib.mpcg_context_solve(self._c, B, C.byref(io)), "mpcg_context_solve")
+        return r
 
 
 def solve_batch_host(pr: MpcgProblem, params: np.ndarray, warm: np.ndarray, xinit: np.ndarray):

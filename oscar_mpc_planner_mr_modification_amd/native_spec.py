@@ -66,7 +66,16 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     return pr
 
 
-EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_solve_batch_device",
-           "mpcg_solve_batch_host", "mpcg_select_best_device")
+class MpcgIo(C.Structure):
+    """Mirror of `mpcg_io` (include/mpcg.h)."""
+    _fields_ = [("params", C.c_void_p), ("warm", C.c_void_p), ("xinit", C.c_void_p), ("lam_in", C.c_void_p),
+                ("xtraj", C.c_void_p), ("utraj", C.c_void_p), ("pobj", C.c_void_p),
+                ("exit_code", C.c_void_p), ("info", C.c_void_p), ("lam_out", C.c_void_p)]
+
+
+ABI_VERSION = 2
+EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
+           "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
+           "mpcg_context_solve", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device")
 
 

@@ -14,7 +14,7 @@ what the reference's host-side modules write before `Solver::solve()`:
                                                      ellipsoid_constraints.cpp:42-56)
 * obstacle ellipsoids, stage k uses prediction k-1 (ellipsoid_constraints.cpp:61-86)
 * consistency parameters on stages 1..N-2           (guidance_constraints.cpp:986-1023)
-* warm start: braking for the non-guided planner    (acados_solver_interface.cpp:528-567)
+* warm start: braking for the non-guided planner    (acados_solver_interface.cpp:303-342)
   and guidance-initialised x, y, psi, v on k=1..N-1 for the guided ones
   (guidance_constraints.cpp:546-570), a/w/spline from the braking warm start.
 
@@ -91,7 +91,7 @@ def _path_eval(coef, starts, s):
 
 
 def _braking(x0, N, dt):
-    """Solver::initializeWithBraking (acados_solver_interface.cpp:528-567)."""
+    """Solver::initializeWithBraking (acados_solver_interface.cpp:303-342)."""
     warm = np.zeros((N + 1, 7))
     x, y, psi, v, s = x0
     a = -abs(DECELERATION)

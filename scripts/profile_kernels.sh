@@ -1,0 +1,19 @@
+#!/bin/bash
+# Kernel-trace statistics and HBM-traffic counters of the bench workload.
+# Run on the GPU box:  bash scripts/profile_kernels.sh <tag>
+# Outputs under gpurun_out/prof_<tag>_{trace,fetch,write,sq}/.  Every pass is a
+# separate process (PMC passes never combined with trace domains).
+set -e
+tag=${1:-latest}
+cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
+o=gpurun_out
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof_${tag}_trace -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $o/prof_${tag}_trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $o/prof_${tag}_fetch -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $o/prof_${tag}_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $o/prof_${tag}_write -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $o/prof_${tag}_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+  -d $o/prof_${tag}_sq -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $o/prof_${tag}_sq.log 2>&1
+echo profile-done

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Summarise a `scripts/profile_kernels.sh <tag>` run into profiles/.
+
+    python scripts/summarize_profile.py <tag> [--config C2 --batch 8192]
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, copied),
+profiles/<tag>_pmc.json (per-kernel counter means) and refreshes
+profiles/traffic_latest.json, which bench.py reads for `roofline.traffic`.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced read, so it is
+doubled.  The correction is cross-checked on select_best_kernel, whose
+algorithmic read volume is known exactly (reported as `calibration`).
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"]
+        key = "sqp_kernel" if "sqp_kernel" in name else ("select_best_kernel" if "select_best" in name else None)
+        if key is None:
+            continue
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        meta[key] = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                       "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--scenes", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=20)
+    args = ap.parse_args()
+    src = os.path.join(ROOT, "gpurun_out")
+    out = os.path.join(ROOT, "profiles")
+    tag = args.tag
+    shutil.copy(os.path.join(src, f"prof_{tag}_trace", "run_kernel_stats.csv"),
+                os.path.join(out, f"{tag}_kernel_stats.csv"))
+    pmc, meta = {}, {}
+    for p in ("fetch", "write", "sq"):
+        f = os.path.join(src, f"prof_{tag}_{p}", "run_counter_collection.csv")
+        if os.path.exists(f):
+            c, m = counters(f)
+            for k, d in c.items():
+                pmc.setdefault(k, {}).update(d)
+            meta.update(m)
+    res = {"tag": tag, "config": args.config, "batch": args.batch, "kernels": {}}
+    for k, d in pmc.items():
+        e = {"counters": d, "launch": meta.get(k, {})}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            e["hbm_read_bytes"] = d["FETCH_SIZE"] * 1024 * 2
+            e["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+            e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+        if "SQ_WAVE_CYCLES" in d:
+            wc = d["SQ_WAVE_CYCLES"]
+            e["shares_of_wave_cycles"] = {c: d[c] / wc for c in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                                                                 "SQ_ACTIVE_INST_LDS", "SQ_WAIT_ANY",
+                                                                 "SQ_WAIT_INST_ANY") if c in d}
+            e["cycles_per_wave"] = 4 * wc / d.get("SQ_WAVES", 1)
+        res["kernels"][k] = e
+    sb = res["kernels"].get("select_best_kernel")
+    if sb and "hbm_read_bytes" in sb:
+        # select_best reads xtraj (B*(N+1)*5 doubles; x, y of stages 1..N-2 touch every line), pobj (B doubles),
+        # exit (B int32), the consistency flags (B bytes) and prev_traj (S*N*2 doubles)
+        algo = 8 * (args.batch * (args.N + 1) * 5 + args.batch) + 4 * args.batch + args.batch + 8 * args.scenes * args.N * 2
+        res["calibration"] = {"kernel": "select_best_kernel", "algorithmic_read_bytes": algo,
+                              "corrected_fetch_bytes": sb["hbm_read_bytes"],
+                              "ratio": sb["hbm_read_bytes"] / algo}
+    json.dump(res, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
+    sq = res["kernels"].get("sqp_kernel", {})
+    if "hbm_bytes_per_launch" in sq:
+        json.dump({"tag": tag, "config": args.config, "batch": args.batch,
+                   "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
+                   "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"]},
+                  open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

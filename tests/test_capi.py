@@ -14,7 +14,8 @@ HDR = os.path.join(ROOT, "include", "mpcg.h")
 
 def declared_functions():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void)\s*\**\s*(mpcg_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void|mpcg_context \*)\s*\**\s*(mpcg_\w+)\s*\(",
+                                 txt, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -28,7 +29,8 @@ def lib():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for n in ("mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device",
-              "mpcg_supported", "mpcg_abi_version", "mpcg_last_error"):
+              "mpcg_supported", "mpcg_abi_version", "mpcg_last_error", "mpcg_solve", "mpcg_context_create",
+              "mpcg_context_solve", "mpcg_context_destroy", "mpcg_problem_from_map", "mpcg_lam_size"):
         assert n in names
 
 
@@ -49,7 +51,7 @@ def test_host_only_queries(lib):
     from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
     from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
     lib.mpcg_abi_version.restype = C.c_int
-    assert lib.mpcg_abi_version() == 1
+    assert lib.mpcg_abi_version() == 2
     for cfg in ("C1", "C2", "C4"):
         pr = problem_from_layout(config_layout(cfg))
         assert lib.mpcg_supported(C.byref(pr)) == 0, cfg
@@ -69,3 +71,60 @@ def test_struct_layout_matches_header():
         for part in decl.split(","):
             names.append(re.sub(r"\[.*\]", "", part).strip())
     assert names == [f[0] for f in MpcgProblem._fields_]
+
+
+def _fields(txt, struct):
+    body = txt[txt.index(f"typedef struct {struct} {{"):txt.index(f"}} {struct};")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = []
+    for decl in re.findall(r"(?:int|double)\s+([^;]+);", body):
+        for part in decl.split(","):
+            names.append(re.sub(r"\[.*\]", "", part).replace("*", "").strip())
+    return names
+
+
+def test_io_struct_layout_matches_header():
+    from oscar_mpc_planner_mr_modification_amd.native_spec import MpcgIo
+    assert _fields(open(HDR).read(), "mpcg_io") == [f[0] for f in MpcgIo._fields_]
+
+
+def _problem_from_map(lib, lay, drop=None, dt=0.2, iters=10):
+    from oscar_mpc_planner_mr_modification_amd.native_spec import UNICYCLE_LB, UNICYCLE_UB, MpcgProblem
+    items = [(k, v) for k, v in lay.pmap.items() if k != drop]
+    names = (C.c_char_p * len(items))(*[k.encode() for k, _ in items])
+    idx = (C.c_int * len(items))(*[v for _, v in items])
+    lb = (C.c_double * 7)(*UNICYCLE_LB)
+    ub = (C.c_double * 7)(*UNICYCLE_UB)
+    pr = MpcgProblem()
+    lib.mpcg_problem_from_map.restype = C.c_int
+    lib.mpcg_last_error.restype = C.c_char_p
+    rc = lib.mpcg_problem_from_map(C.byref(pr), lay.N, lay.npar, len(items), names, idx, lb, ub,
+                                   C.c_double(dt), iters)
+    return rc, pr
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+def test_problem_from_parameter_map_matches_layout(lib, cfg):
+    """mpcg_problem_from_map (what the C++ Solver calls on parameter_map.yaml)
+    reproduces the Python layout's problem field by field."""
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
+    lay = config_layout(cfg)
+    rc, pr = _problem_from_map(lib, lay)
+    assert rc == 0
+    ref = problem_from_layout(lay)
+    for name, _ in ref._fields_:
+        a, b = getattr(pr, name), getattr(ref, name)
+        if hasattr(a, "__len__"):
+            assert list(a) == list(b), name
+        else:
+            assert a == b, name
+
+
+def test_problem_from_map_reports_missing_entries(lib):
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    rc, _ = _problem_from_map(lib, config_layout("C2"), drop="contour")
+    assert rc == -1
+    assert b"contour" in lib.mpcg_last_error()
+    rc, _ = _problem_from_map(lib, config_layout("C2"), drop="ellipsoid_obst_3_r")
+    assert rc == -1 and b"obstacle 3" in lib.mpcg_last_error()

@@ -76,7 +76,7 @@ def test_parity_c4_horizon30(native, torch_dev, oracle_mod):
 
 
 def test_single_rti_iteration(native, torch_dev, oracle_mod):
-    """one SQP-RTI iteration == solver_type SQP path (acados_solver_interface.cpp:253-254)"""
+    """one SQP-RTI iteration == solver_type SQP path (acados_solver_interface.cpp:28-29)"""
     lay, b, ref, got = _run(native, torch_dev, oracle_mod, "C2", 4, 8, 99, sqp_iters=1)
     _compare(ref, got, "C2 sqp_iters=1", require_success=False)
 
@@ -138,3 +138,60 @@ def test_select_best_matches_reference_rule(native, torch_dev, oracle_mod):
                                       prev_sel, 0.8, disabled)
     assert np.array_equal(best.cpu().numpy(), hb)
     np.testing.assert_allclose(obj.cpu().numpy(), hobj, rtol=1e-12, atol=1e-12)
+
+
+def test_multipliers_carried_between_solves(native, torch_dev, oracle_mod):
+    """Two consecutive control steps of the same planners: the second solve
+    starts from the NLP multipliers the first one left in the capsule
+    (mpcg_io lam_in/lam_out; acados_solver_interface.cpp:86-119, reset on
+    failure :186-190).  GPU and oracle agree on both steps and on the
+    multipliers themselves."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+    lay = config_layout("C2")
+    b = make_batch(lay, 8, 8, seed=515)
+    orc = oracle_mod.Oracle(lay)
+    pr = native.problem_from_layout(lay)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(torch_dev)  # noqa: E731
+    ref1 = orc.solve_batch(b.params, b.warm, b.xinit, return_lam=True)
+    out1 = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), lam_out=True)
+    got1 = {k: v.cpu().numpy() for k, v in out1.items()}
+    _compare(ref1, got1, "step 1")
+    ok = (got1["exit"] == 1)
+    lam_err = np.abs(got1["lam"][ok] - ref1["lam"][ok]).max()
+    lam_scale = max(1.0, np.abs(ref1["lam"][ok]).max())
+    assert lam_err <= 1e-6 * lam_scale, lam_err
+    # the wrapper's rule: a failed solve resets the capsule -> zero multipliers
+    lam2 = np.where(ok[:, None, None], ref1["lam"], 0.0)
+    ref2 = orc.solve_batch(b.params, b.warm, b.xinit, lam_in=lam2, return_lam=True)
+    out2 = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), lam_in=t(lam2), lam_out=True)
+    got2 = {k: v.cpu().numpy() for k, v in out2.items()}
+    _compare(ref2, got2, "step 2 (carried multipliers)")
+    # carrying multipliers changes the first exact-Hessian linearisation
+    assert np.abs(ref2["xtraj"] - ref1["xtraj"]).max() > 1e-6
+
+
+def test_context_host_path_matches_device_path(native, torch_dev, oracle_mod):
+    """mpcg_context_* (what one drop-in Solver holds) == mpcg_solve on device."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+    lay = config_layout("C2")
+    b = make_batch(lay, 3, 8, seed=616)
+    pr = native.problem_from_layout(lay)
+    ctx = native.Context(pr, max_batch=32)
+    r = ctx.solve(b.params, b.warm, b.xinit, lam_out=True)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(torch_dev)  # noqa: E731
+    out = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), lam_out=True)
+    torch.cuda.synchronize()
+    for k in ("xtraj", "utraj", "pobj", "exit", "info", "lam"):
+        np.testing.assert_array_equal(r[k], out[k].cpu().numpy(), err_msg=k)
+    # batch of one, reusing the context (one Solver::solve())
+    r1 = ctx.solve(b.params[5:6], b.warm[5:6], b.xinit[5:6])
+    np.testing.assert_array_equal(r1["xtraj"][0], r["xtraj"][5])
+    with pytest.raises(RuntimeError):
+        ctx.solve(np.zeros((33, lay.N, lay.npar)), np.zeros((33, lay.N + 1, 7)), np.zeros((33, 5)))
+    ctx.close()
