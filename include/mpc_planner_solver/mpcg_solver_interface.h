@@ -1,0 +1,169 @@
+// mpcg_solver_interface.h — drop-in `MPCPlanner::Solver` over the MI355X backend.
+//
+// Same public surface as the reference's acados Solver
+// (mpc_planner_solver/include/mpc_planner_solver/acados_solver_interface.h:51-222):
+// the per-solver buffers (AcadosParameters / AcadosInfo / AcadosOutput with
+// the reference's member names and layouts), the dimensions, the YAML maps,
+// and every method the planner and the modules call.  A solve runs the
+// batched HIP SQP kernel (libmpcg.so, include/mpcg.h) on batch 1, or on all
+// guesses at once through SolverBatch (the replacement of the OpenMP fan-out
+// in GuidanceConstraints::optimize, guidance_constraints.cpp:304-421; see
+// INTEGRATION.md).
+//
+// Compile-time dimensions come from the generated mpcg_solver_dims.h
+// (SOLVER_N, SOLVER_NP, SOLVER_NX, SOLVER_NU), as the reference takes them
+// from the generated acados_solver_Solver.h.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "mpc_planner_solver/mpcg_config.h"
+#include "mpc_planner_solver/mpcg_solver_dims.h"
+#include "mpc_planner_solver/state.h"
+#include "mpcg.h"
+
+namespace MPCPlanner {
+
+// Input block of one solve (acados_solver_interface.h:51-90).
+struct AcadosParameters {
+    double xinit[SOLVER_NX];                                   // initial state
+    double x0[(SOLVER_NU + SOLVER_NX) * (SOLVER_N + 1)];       // warm start [u0 x0 | u1 x1 | ... | uN xN]
+    double all_parameters[SOLVER_NP * SOLVER_N];               // horizon-major: [k * SOLVER_NP + index]
+    double solver_timeout{0.};                                 // accepted, not used (fixed iteration count)
+
+    double* getU0() { return x0; }
+
+    AcadosParameters();
+    void printParameters(const mpcg::YamlNode& parameter_map) const;
+};
+
+class Solver {
+public:
+    // acados_solver_interface.h:96-124
+    struct AcadosInfo {
+        double min_time = 1e12;
+        double kkt_norm_inf = 0.;
+        double elapsed_time = 0.;
+        int sqp_iter = 0;
+        double nlp_res = 0.;
+        double solvetime = 0.;
+        int qp_status = 0;        // HPIPM convention: 0 ok, 1 max-iter, 2 min-step, 3 nan
+        double pobj{0.};
+        int qp_iter = 0;          // total interior-point iterations of the last solve (extra)
+        void print() const;
+    };
+
+    // acados_solver_interface.h:126-148
+    struct AcadosOutput {
+        double xtraj[SOLVER_NX * (SOLVER_N + 1)];
+        double utraj[SOLVER_NU * SOLVER_N];
+        AcadosOutput();
+        void print() const;
+    };
+
+    int _solver_id;
+
+    AcadosParameters _params;
+    AcadosInfo _info;
+    AcadosOutput _output;
+
+    int N;
+    unsigned int nu;
+    unsigned int nx;
+    unsigned int nvar;
+    unsigned int npar;
+    double dt;
+
+    mpcg::YamlNode _config, _parameter_map, _model_map;
+
+    int _num_iterations;
+
+    explicit Solver(int solver_id = 0);
+    ~Solver();
+    Solver(const Solver&) = delete;
+
+    // Copies the parameters only (acados_solver_interface.cpp:67-77): the
+    // multipliers this solver kept from its own previous solve stay.
+    Solver& operator=(const Solver& rhs);
+
+    void reset();
+
+    int solve();
+
+    // One iteration at a time (acados_solver_interface.cpp:121-204)
+    void initializeOneIteration();
+    int solveOneIteration();
+    int completeOneIteration();
+
+    // PARAMETERS
+    bool hasParameter(std::string&& parameter);
+    void setParameter(int k, std::string&& parameter, double value);
+    void setParameter(int k, std::string& parameter, double value);
+    double getParameter(int k, std::string&& parameter);
+
+    // XINIT
+    void setXinit(std::string&& state_name, double value);
+    void setXinit(const State& state);
+
+    // WARMSTART
+    void setEgoPrediction(unsigned int k, std::string&& var_name, double value);
+    double getEgoPrediction(unsigned int k, std::string&& var_name);
+    void setEgoPredictionPosition(unsigned int k, const Vec2& value);
+    Vec2 getEgoPredictionPosition(unsigned int k);
+
+    void loadWarmstart();
+    void initializeWarmstart(const State& state, bool shift_previous_solution_forward);
+    void initializeWithState(const State& initial_state);
+    void initializeWithBraking(const State& initial_state);
+
+    // OUTPUT
+    double getOutput(int k, std::string&& state_name) const;
+
+    // DEBUG
+    std::string explainExitFlag(int exitflag) const;
+    void printIfBoundLimited() const;
+
+    // ---- backend access (not in the reference surface)
+    const mpcg_problem& problem() const { return _problem; }
+    // NLP multipliers carried between solves, [N][nx + nh] (include/mpcg.h, mpcg_io)
+    std::vector<double>& multipliers() { return _lam; }
+
+private:
+    friend class SolverBatch;
+    mpcg_problem _problem;
+    mpcg_context* _ctx = nullptr;   // created on the first solve (no GPU needed before)
+    std::vector<double> _iterate;   // NLP iterate [u x] per stage, what loadWarmstart loads (ocp_nlp_out x/u)
+    std::vector<double> _lam;       // ocp_nlp_out multipliers
+    int _exit_code_one_iter = -1;
+    int _raw_status = 0;            // kernel exit code of the last call (already mapped to the 1/0/2/3/4 convention)
+
+    int run(int iterations);
+    void absorb(const double* xtraj, const double* utraj, double pobj, int exit_code, const int* info,
+                const double* lam);
+    int model_index(const std::string& name) const;
+    bool is_state(const std::string& name) const;
+};
+
+// All guesses of one GuidanceConstraints::optimize call in one launch.
+// solve() is equivalent to calling Solver::solve() on each solver in turn
+// (same results, same side effects on each solver's outputs, info and
+// multipliers) and returns their exit codes.
+class SolverBatch {
+public:
+    SolverBatch(const Solver& prototype, int max_batch);
+    ~SolverBatch();
+    SolverBatch(const SolverBatch&) = delete;
+    SolverBatch& operator=(const SolverBatch&) = delete;
+
+    std::vector<int> solve(const std::vector<Solver*>& solvers);
+
+private:
+    mpcg_problem _problem;
+    int _max_batch;
+    mpcg_context* _ctx = nullptr;
+    std::vector<double> _params, _warm, _xinit, _lam_in, _xtraj, _utraj, _pobj, _lam_out;
+    std::vector<int> _exit, _info;
+};
+
+}  // namespace MPCPlanner

@@ -116,6 +116,9 @@ mpcg_context *mpcg_context_create(const mpcg_problem *pr, int max_batch);
 void mpcg_context_destroy(mpcg_context *ctx);
 /* host pointers; synchronous.  Returns 0, or < 0 with mpcg_last_error(). */
 int mpcg_context_solve(mpcg_context *ctx, int batch, const mpcg_io *io);
+/* SQP-RTI iterations of the next mpcg_context_solve calls (1 = one
+ * solveOneIteration(), acados_solver_interface.cpp:145-160).  Returns 0. */
+int mpcg_context_set_iterations(mpcg_context *ctx, int sqp_iters);
 
 /* 0 if (N, n_lin, n_ell) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);

@@ -15,6 +15,10 @@ ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["mpcg_kernels.hip"]
 HEADERS = ["mpcg_device.h", "mpcg_sqp.h"]
+HOST_SOURCES = ["host/mpcg_yaml.cpp", "host/mpcg_solver.cpp"]
+HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_config.h", "mpc_planner_solver/state.h",
+                "mpc_planner_solver/mpcg_solver_interface.h", "mpc_planner_solver/solver_interface.h"]
+BUILD = os.path.join(PKG, "build")
 
 
 def _stale(target, deps):
@@ -37,5 +41,41 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_cpp(config: str = "C2", force: bool = False, verbose: bool = False) -> dict:
+    """The drop-in C++ MPCPlanner::Solver for one generated solver
+    (dimensions are compile-time, as in the reference): codegen into
+    build/<config>/, then libmpc_planner_solver.so and the test program
+    tests/cpp/test_solver.cpp linked against libmpcg.so."""
+    from . import codegen
+    from .layouts import config_layout
+
+    lib_mpcg = build_lib()
+    out = os.path.join(BUILD, config)
+    codegen.generate(config_layout(config), out)
+    so = os.path.join(out, "libmpc_planner_solver.so")
+    exe = os.path.join(out, "test_solver")
+    srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES] + [os.path.join(out, "mpc_planner_parameters.cpp")]
+    deps = srcs + [os.path.join(INCLUDE, h) for h in HOST_HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), lib_mpcg,
+                                                                     __file__]
+    inc = [f"-I{os.path.join(out, 'include')}", f"-I{INCLUDE}"]
+    if force or _stale(so, deps):
+        cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra"] + inc + srcs + \
+              ["-o", so + ".tmp", f"-L{PKG}", "-lmpcg", f"-Wl,-rpath,{PKG}"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(so + ".tmp", so)
+    test_src = os.path.join(ROOT, "tests", "cpp", "test_solver.cpp")
+    if os.path.exists(test_src) and (force or _stale(exe, [test_src, so])):
+        cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra"] + inc + [test_src, "-o", exe, f"-L{out}",
+                                                                      "-lmpc_planner_solver", f"-L{PKG}", "-lmpcg",
+                                                                      f"-Wl,-rpath,{out}:{PKG}"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return {"dir": out, "lib": so, "test": exe}
+
+
 if __name__ == "__main__":
     print(build_lib(force=True, verbose=True))
+    print(build_cpp("C2", force=True, verbose=True))

@@ -262,6 +262,12 @@ void mpcg_context_destroy(mpcg_context* c) {
     delete c;
 }
 
+int mpcg_context_set_iterations(mpcg_context* c, int sqp_iters) {
+    if (!c || sqp_iters < 1) { mpcg::g_err = "invalid arguments"; return -1; }
+    c->pr.sqp_iters = sqp_iters;
+    return 0;
+}
+
 int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
     if (!c || !io || batch < 0 || batch > c->max_batch) {
         mpcg::g_err = "mpcg_context_solve: invalid arguments or batch > max_batch";

@@ -45,6 +45,7 @@ def _load():
     lib.mpcg_context_create.restype = vp
     lib.mpcg_context_destroy.argtypes = [vp]
     lib.mpcg_context_solve.argtypes = [vp, C.c_int, C.POINTER(MpcgIo)]
+    lib.mpcg_context_set_iterations.argtypes = [vp, C.c_int]
     lib.mpcg_solve_batch_device.argtypes = [P, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcg_solve_batch_device.restype = C.c_int
     lib.mpcg_solve_batch_host.argtypes = [P, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -132,6 +133,9 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_iterations(self, sqp_iters: int):
+        _check(lib.mpcg_context_set_iterations(self._c, sqp_iters), "mpcg_context_set_iterations")
 
     def solve(self, params, warm, xinit, lam_in=None, lam_out=False):
         pr = self.pr

@@ -76,6 +76,6 @@ class MpcgIo(C.Structure):
 ABI_VERSION = 2
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
            "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
-           "mpcg_context_solve", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device")
+           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device")
 
 
