@@ -20,6 +20,31 @@ namespace mpcg {
 constexpr int NX = MPCG_NX, NU = MPCG_NU, NZ = MPCG_NVAR;
 
 // ---------------------------------------------------------------------------
+// fp64 reciprocal / reciprocal square root: the hardware estimate
+// (v_rcp_f64 / v_rsq_f64) refined by two Newton steps, within an ulp of the
+// correctly rounded result at a third of the latency of the IEEE division /
+// square-root expansions.  Arguments are finite and non-zero (positive for
+// frsq) wherever they are used.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double frcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
+__device__ __forceinline__ double frsq(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    return y * fma(-h * y, y, 1.5);
+}
+
+// sqrt for x > 0
+__device__ __forceinline__ double fsqrt_pos(double x) { return x * frsq(x); }
+
+// ---------------------------------------------------------------------------
 // glued spline of spline.py:39-58: for both axes the glued position G and the
 // glued segment-derivative D, each with first and second s-derivatives.
 // ---------------------------------------------------------------------------
@@ -53,7 +78,7 @@ __device__ inline void spline_jets(const mpcg_problem& pr, const double* __restr
         // lambda_k uses the start of segment k (spline.py:37)
         const double sk = base[9 * k + 8];
         const double e = exp((s - sk + 0.02) / 0.1);
-        const double l0 = 1.0 / (1.0 + e);
+        const double l0 = frcp(1.0 + e);
         const double l1 = -10.0 * l0 * (1.0 - l0);
         const double l2 = 100.0 * l0 * (1.0 - l0) * (1.0 - 2.0 * l0);
         const double* seg = base + 9 * (k - 1);
@@ -97,8 +122,8 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
     double L = wa * a * a + ww * w * w + wv * (v - vref) * (v - vref);
     SplineJets J;
     spline_jets(pr, p, s, J);
-    const double r = sqrt(J.Dx[0] * J.Dx[0] + J.Dy[0] * J.Dy[0]);
-    const double ir = 1.0 / r;
+    const double rsq = J.Dx[0] * J.Dx[0] + J.Dy[0] * J.Dy[0];
+    const double ir = frsq(rsq);
     const double tx = J.Dx[0] * ir, ty = J.Dy[0] * ir;
     const double ex = x - J.Gx[0], ey = y - J.Gy[0];
     const double ec = ty * ex - tx * ey;  // contour error (contouring.py:166)
@@ -249,13 +274,17 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NZ], 
 // offset) cost only their own rotations.
 // ---------------------------------------------------------------------------
 __device__ inline void mirror7(double A[NZ][NZ], double eps) {
+    // Cyclic Jacobi on the symmetric part, one-sided rotation updates on the
+    // upper triangle (a_pp -= t a_pq, a_qq += t a_pq, off-diagonal pairs with
+    // tau = s / (1 + c)); V accumulates the eigenvectors.  Then
+    // A = V diag(f(d)) V' with f(d) = eps if |d| <= eps else |d|.
     double V[NZ][NZ];
 #pragma unroll
     for (int i = 0; i < NZ; ++i)
 #pragma unroll
         for (int j = 0; j < NZ; ++j) {
             V[i][j] = (i == j) ? 1.0 : 0.0;
-            if (j > i) { double m = 0.5 * (A[i][j] + A[j][i]); A[i][j] = m; A[j][i] = m; }
+            if (j > i) A[i][j] = 0.5 * (A[i][j] + A[j][i]);
         }
     for (int sweep = 0; sweep < 50; ++sweep) {
         double off = 0.0, dia = 0.0;
@@ -272,26 +301,30 @@ __device__ inline void mirror7(double A[NZ][NZ], double eps) {
             for (int q = p + 1; q < NZ; ++q) {
                 const double apq = A[p][q];
                 if (fabs(apq) >= 1e-300) {
-                    const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-                    const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                    const double theta = 0.5 * (A[q][q] - A[p][p]) * frcp(apq);
+                    const double at = fabs(theta);
+                    // t = 1 / (|theta| + sqrt(theta^2 + 1)); ~1 / (2 |theta|) once theta^2 would overflow
+                    double t = at < 1e150 ? frcp(at + fsqrt_pos(fma(at, at, 1.0))) : 0.5 * frcp(at);
+                    t = theta >= 0.0 ? t : -t;
+                    const double c = frsq(fma(t, t, 1.0)), sn = t * c;
+                    const double tau = sn * frcp(1.0 + c);
+                    A[p][p] -= t * apq;
+                    A[q][q] += t * apq;
+                    A[p][q] = 0.0;
 #pragma unroll
-                    for (int k = 0; k < NZ; ++k) {
-                        const double akp = A[k][p], akq = A[k][q];
-                        A[k][p] = c * akp - s * akq;
-                        A[k][q] = s * akp + c * akq;
+                    for (int r = 0; r < NZ; ++r) {
+                        if (r == p || r == q) continue;
+                        double& arp = r < p ? A[r][p] : A[p][r];
+                        double& arq = r < q ? A[r][q] : A[q][r];
+                        const double g = arp, h = arq;
+                        arp = g - sn * fma(g, tau, h);
+                        arq = h + sn * fma(-h, tau, g);
                     }
 #pragma unroll
-                    for (int k = 0; k < NZ; ++k) {
-                        const double apk = A[p][k], aqk = A[q][k];
-                        A[p][k] = c * apk - s * aqk;
-                        A[q][k] = s * apk + c * aqk;
-                    }
-#pragma unroll
-                    for (int k = 0; k < NZ; ++k) {
-                        const double vkp = V[k][p], vkq = V[k][q];
-                        V[k][p] = c * vkp - s * vkq;
-                        V[k][q] = s * vkp + c * vkq;
+                    for (int r = 0; r < NZ; ++r) {
+                        const double g = V[r][p], h = V[r][q];
+                        V[r][p] = g - sn * fma(g, tau, h);
+                        V[r][q] = h + sn * fma(-h, tau, g);
                     }
                 }
             }

@@ -196,7 +196,7 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             const double chi = sqrt(o[5]);
             const double ra = o[3] * chi + rdisc + o[6];
             const double rb = o[4] * chi + rdisc + o[6];
-            const double D0 = 1.0 / (ra * ra), D1 = 1.0 / (rb * rb);
+            const double D0 = frcp(ra * ra), D1 = frcp(rb * rb);
             double so, co;
             sincos(o[2], &so, &co);
             const double M00 = co * co * D0 + so * so * D1;
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const double rin = row_dot<C, CL>(S.Dg[kc], s, hoff, dzk) + t -
                                            row_gap<C, CL>(pr, zk, S.hd[kc], s, hoff);
                         R.rin[s] = rin;
-                        R.it[s] = 1.0 / t;
+                        R.it[s] = frcp(t);
                         ri = fmax(ri, fabs(rin));
                         comp += l * t;
                     }
@@ -572,12 +572,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         __syncthreads();
                         if (lane < 15) {
                             const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
-                            const double l00 = sqrt(m00);
-                            const double il00 = 1.0 / l00;
+                            // 2x2 Cholesky through reciprocal square roots
+                            const double il00 = frsq(m00);
+                            const double l00 = m00 * il00;
                             const double l10 = m10 * il00;
                             const double r11 = m11 - l10 * l10;
-                            const double l11 = sqrt(r11);
-                            const double il11 = 1.0 / l11;
+                            const double il11 = frsq(r11);
                             if (!(m00 > 0.0) || !(r11 > 0.0)) S.flag = 1;
                             const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
                             const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
@@ -742,11 +742,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double dt, dl;
                             row_step(Cc, hoff, s, dt, dl);
                             rmax = fmax(rmax, -dt * R.it[s]);
-                            if (dl < 0.0) rmax = fmax(rmax, -dl / R.l[s]);
+                            if (dl < 0.0) rmax = fmax(rmax, -dl * frcp(R.l[s]));
                         }
                     });
                     rmax = wave_max(rmax);
-                    const double amax = rmax > 0.0 ? 1.0 / rmax : 1e300;
+                    const double amax = rmax > 0.0 ? frcp(rmax) : 1e300;
                     if (phase == 0) {
                         const double aa = fmin(amax, 1.0);
                         double ca = 0.0;
