@@ -180,15 +180,20 @@ def main():
             agree += int((ref["status"] == exit_h[sl]).sum())
             compared += len(ref["status"])
             done = sl.stop
-        tc = time.perf_counter()
-        n1 = 64
-        orc.solve_batch(b.params[:n1], b.warm[:n1], b.xinit[:n1], nthreads=1)
-        t1 = time.perf_counter() - tc
+        # also 1 thread and 8 threads (the reference's num_threads(8))
+        def rate(n, nthreads):
+            tc = time.perf_counter()
+            orc.solve_batch(b.params[:n], b.warm[:n], b.xinit[:n], nthreads=nthreads)
+            return n / (time.perf_counter() - tc)
+
+        r1 = rate(64, 1)
+        r8 = rate(512, 8) if threads >= 8 else None
         result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
                                   "kind": "port",
                                   "sample": f"first {done} of the {B} solves of this batch, C oracle "
                                             f"(same algorithm), OpenMP {threads} threads",
-                                  "single_thread_solves_per_s": round(n1 / t1, 2)}
+                                  "single_thread_solves_per_s": round(r1, 2),
+                                  "eight_thread_solves_per_s": None if r8 is None else round(r8, 2)}
         result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
                             "solves_compared": compared, "tolerance": 1e-4}
         result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)

@@ -551,6 +551,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                     for (int m = 0; m < NX; ++m) { fi[m] = S.F[N - 1][m][ei]; fj[m] = S.F[N - 1][m][ej]; }
                     hv = S.H[N - 1][le] + (dhd >= 0 ? S.dH[N - 1][dhd] : 0.0) + (dhb >= 0 ? S.dH[N - 1][dhb] : 0.0);
+#pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
                         double Pm[15];
 #pragma unroll
@@ -637,6 +638,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double pu[NX], pmine[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) { pu[i] = S.q[N][NU + i]; pmine[i] = pu[i]; }
+                    #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
                         double pn[NX];
 #pragma unroll
@@ -664,6 +666,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                     for (int i = 0; i < NX; ++i) e[i] = S.rdyn[kq][i] + S.F[kq][i][0] * kf0 + S.F[kq][i][1] * kf1;
                     double dxu[NX] = {0, 0, 0, 0, 0}, dxmine[NX] = {0, 0, 0, 0, 0};
+                    #pragma unroll
                     for (int kk = 0; kk < N; ++kk) {
                         double dn[NX];
 #pragma unroll
