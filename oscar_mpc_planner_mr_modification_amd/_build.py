@@ -13,8 +13,10 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libmpcg.so")
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["mpcg_kernels.hip"]
-HEADERS = ["mpcg_device.h", "mpcg_sqp.h"]
+# source -> extra flags.  The producers are compiled without floating-point
+# contraction so that they agree bit for bit with the host restatement.
+SOURCES = {"mpcg_kernels.hip": [], "mpcg_prepare.hip": ["-ffp-contract=off"]}
+HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h"]
 HOST_SOURCES = ["host/mpcg_yaml.cpp", "host/mpcg_solver.cpp"]
 HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_config.h", "mpc_planner_solver/state.h",
                 "mpc_planner_solver/mpcg_solver_interface.h", "mpc_planner_solver/solver_interface.h"]
@@ -28,17 +30,31 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), __file__]
-    if not force and not _stale(LIB, deps):
-        return LIB
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           f"-I{INCLUDE}", f"-I{CSRC}", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: str = LIB) -> str:
+    deps = [os.path.join(CSRC, s) for s in list(SOURCES) + HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), __file__]
+    if not force and not _stale(out, deps):
+        return out
+    objdir = os.path.join(BUILD, "obj" + ("_" + "_".join(f.strip("-").replace("=", "") for f in extra_flags)
+                                          if extra_flags else ""))
+    os.makedirs(objdir, exist_ok=True)
+    common = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}"]
+    objs, procs = [], []
+    for src, flags in SOURCES.items():
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        cmd = common + list(flags) + list(extra_flags) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    for p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, "hipcc")
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def build_cpp(config: str = "C2", force: bool = False, verbose: bool = False) -> dict:

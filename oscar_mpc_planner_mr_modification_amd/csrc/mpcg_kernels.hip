@@ -66,7 +66,7 @@ __global__ void select_best_kernel(int n_scenes, int G, int N, const double* __r
 }
 
 // ---- dispatch over compiled instances ------------------------------------
-static thread_local std::string g_err;
+thread_local std::string g_err;  // also set by mpcg_prepare.hip
 static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG_STAMPS builds only)
 
 template <class C>

@@ -1,0 +1,222 @@
+// mpcg_prepare.h — per-guess solver inputs of one control step on the GPU
+// (SURVEY §8f rows 1-3): the host-side module steps that run before every
+// Solver::solve() in GuidanceConstraints::optimize, for all scenes x planners
+// at once.  Host restatement and semantics: producers.py; ABI: include/mpcg.h
+// (mpcg_prepare).
+//
+// One workgroup (64 lanes) per (scene, planner):
+//   warm start   main warm start (or the braking plan, acados_solver_interface.cpp:303-342),
+//                guided planners: x, y, psi, v from the guidance trajectory at k dt, k = 1..N-1
+//                (initializeSolverWithGuidance, guidance_constraints.cpp:546-570)
+//   halfspaces   lane k-1 runs LinearizedConstraints::update for stage k: 3 Douglas-Rachford
+//                rounds over all obstacles (linearized_constraints.cpp:130-148), then
+//                a = (o - p) / |o - p|, b = a.o - (1e-3 + r_robot) (:84-105);
+//                non-guided planner: dummies (a1 = 1, a2 = 0, b = x + 100)
+//   ellipsoids   stage 0 dummies, stage k prediction k-1 (ellipsoid_constraints.cpp:34-86)
+//   consistency  interpolated previous plan (guidance_constraints.cpp:1073-1133) on stages
+//                1..N-2 of the planners with the consistency cost (:986-1023)
+// then all lanes stream the N x npar parameter block out with coalesced stores.
+// Compiled only into mpcg_prepare.hip, with -ffp-contract=off (no fused
+// multiply-adds), and written in the host restatement's operation order, so
+// the halfspace, ellipsoid and consistency values agree bit for bit with
+// producers.py / the test oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcg.h"
+
+namespace mpcg {
+
+constexpr int PREP_MAX_N = 32;
+constexpr int PREP_MAX_OBS = 24;
+
+__device__ __forceinline__ double norm2_rn(double dx, double dy) {
+    return __dsqrt_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)));
+}
+
+// ros_tools DouglasRachford: project onto the outside of the disc (c, r) along c -> start
+__device__ __forceinline__ void dr_project_disc(double px, double py, double cx, double cy, double r, double sx,
+                                                double sy, double& ox, double& oy) {
+    if (norm2_rn(__dsub_rn(px, cx), __dsub_rn(py, cy)) < r) {
+        const double dx = __dsub_rn(sx, cx), dy = __dsub_rn(sy, cy);
+        const double n = norm2_rn(dx, dy);
+        ox = __dadd_rn(cx, __dmul_rn(__ddiv_rn(dx, n), r));
+        oy = __dadd_rn(cy, __dmul_rn(__ddiv_rn(dy, n), r));
+    } else {
+        ox = px;
+        oy = py;
+    }
+}
+
+__device__ __forceinline__ void dr_reflect(double px, double py, double cx, double cy, double r, double sx,
+                                           double sy, double& ox, double& oy) {
+    double qx, qy;
+    dr_project_disc(px, py, cx, cy, r, sx, sy, qx, qy);
+    ox = __dsub_rn(__dmul_rn(2.0, qx), px);
+    oy = __dsub_rn(__dmul_rn(2.0, qy), py);
+}
+
+struct PrepLds {
+    double warm[PREP_MAX_N + 1][MPCG_NVAR];
+    double lin[PREP_MAX_N][PREP_MAX_OBS][3];
+    double prev[PREP_MAX_N][2];
+    int prev_ok;
+};
+
+__global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scenes, int G, mpcg_scene_io in,
+                                                     double* __restrict__ params, double* __restrict__ warm,
+                                                     double* __restrict__ xinit, double* __restrict__ prev_out,
+                                                     unsigned char* __restrict__ cons_active) {
+    __shared__ PrepLds L;
+    const int sol = blockIdx.x;
+    const int sc = sol / G, g = sol - sc * G;
+    if (sc >= n_scenes) return;
+    const int lane = threadIdx.x;
+    const int N = pr.N, npar = pr.npar, NL = pr.n_lin, NE = pr.n_ell;
+    const double dt = pr.dt;
+    const double* st = in.state + (size_t)sc * MPCG_NX;
+    const bool guided = in.guided && in.guided[(size_t)sc * G + g];
+    const double x0 = st[0], y0 = st[1];
+
+    // ---- main warm start (copied into every planner: *solver = *_solver)
+    if (in.main_warm) {
+        const double* mw = in.main_warm + (size_t)sc * (N + 1) * MPCG_NVAR;
+        for (int e = lane; e < (N + 1) * MPCG_NVAR; e += 64) (&L.warm[0][0])[e] = mw[e];
+    } else if (lane == 0) {
+        // Solver::initializeWithBraking
+        double x = st[0], y = st[1], psi = st[2], v = st[3], s = st[4];
+        const double a = -fabs(in.deceleration);
+        const double c = cos(psi), sn = sin(psi);
+        double* w = L.warm[0];
+        w[0] = a; w[1] = 0.0; w[2] = x; w[3] = y; w[4] = psi; w[5] = v; w[6] = s;
+        for (int k = 1; k <= N; ++k) {
+            x = __dadd_rn(x, __dmul_rn(__dmul_rn(v, dt), c));
+            y = __dadd_rn(y, __dmul_rn(__dmul_rn(v, dt), sn));
+            s = __dadd_rn(s, __dmul_rn(v, dt));
+            v = fmax(__dadd_rn(v, __dmul_rn(a, dt)), 0.0);
+            w = L.warm[k];
+            w[0] = a; w[1] = 0.0; w[2] = x; w[3] = y; w[4] = psi; w[5] = v; w[6] = s;
+        }
+    }
+    __syncthreads();
+    // ---- initializeSolverWithGuidance (k = 1..N-1)
+    if (guided && lane >= 1 && lane < N) {
+        const double* gk = in.guidance + (((size_t)sc * G + g) * (N + 1) + lane) * 4;
+        L.warm[lane][2] = gk[0];
+        L.warm[lane][3] = gk[1];
+        L.warm[lane][4] = atan2(gk[3], gk[2]);
+        L.warm[lane][5] = norm2_rn(gk[2], gk[3]);
+    }
+    __syncthreads();
+    // ---- topology halfspaces, lane k-1 <-> stage k
+    const int n_obs = NL < NE ? NL : NE;
+    const double rr = __dadd_rn(1e-3, in.robot_radius);
+    if (guided && lane < N - 1 && n_obs > 0) {
+        const int k = lane + 1;
+        const double* ob = in.obst + (size_t)sc * NE * N * 5;  // [i][j][5]
+        auto opos = [&](int i, double& ox, double& oy) {
+            const double* o = ob + ((size_t)i * N + (k - 1)) * 5;
+            ox = o[0];
+            oy = o[1];
+        };
+        double px = L.warm[k][2], py = L.warm[k][3];
+        double ax, ay;
+        opos(0, ax, ay);
+        for (int it = 0; it < 3; ++it)
+            for (int i = 0; i < n_obs; ++i) {
+                double cx, cy, fx, fy, rx, ry;
+                opos(i, cx, cy);
+                dr_reflect(px, py, ax, ay, rr, px, py, fx, fy);
+                dr_reflect(fx, fy, cx, cy, rr, px, py, rx, ry);
+                px = __dmul_rn(0.5, __dadd_rn(px, rx));
+                py = __dmul_rn(0.5, __dadd_rn(py, ry));
+            }
+        for (int i = 0; i < n_obs; ++i) {
+            double ox, oy;
+            opos(i, ox, oy);
+            const double dx = __dsub_rn(ox, px), dy = __dsub_rn(oy, py);
+            const double dist = norm2_rn(dx, dy);
+            const double a1 = __ddiv_rn(dx, dist), a2 = __ddiv_rn(dy, dist);
+            L.lin[k][i][0] = a1;
+            L.lin[k][i][1] = a2;
+            L.lin[k][i][2] = __dsub_rn(__dadd_rn(__dmul_rn(a1, ox), __dmul_rn(a2, oy)), rr);
+        }
+    }
+    // ---- previous plan interpolated by the elapsed time
+    if (lane == 0) {
+        int ok = 0;
+        if (in.prev_traj && in.prev_elapsed) {
+            const double el = in.prev_elapsed[sc];
+            if (isfinite(el)) {
+                const int k_shift = (int)floor(__ddiv_rn(el, dt));
+                ok = k_shift < N - 1;
+            }
+        }
+        L.prev_ok = ok;
+    }
+    __syncthreads();
+    const bool prev_ok = L.prev_ok != 0;
+    if (prev_ok && lane < N) {
+        const double* pv = in.prev_traj + (size_t)sc * N * 2;
+        const double el = in.prev_elapsed[sc];
+        const int k_shift = (int)floor(__ddiv_rn(el, dt));
+        const double alpha = __ddiv_rn(__dsub_rn(el, __dmul_rn((double)k_shift, dt)), dt);
+        const int src = lane + k_shift;
+        for (int c = 0; c < 2; ++c) {
+            double v;
+            if (src < N - 1) {
+                v = __dadd_rn(__dmul_rn(__dsub_rn(1.0, alpha), pv[src * 2 + c]), __dmul_rn(alpha, pv[(src + 1) * 2 + c]));
+            } else if (src == N - 1) {
+                v = pv[(N - 1) * 2 + c];
+            } else {
+                const double vel = __ddiv_rn(__dsub_rn(pv[(N - 1) * 2 + c], pv[(N - 2) * 2 + c]), dt);
+                const double extra = __dadd_rn(__dmul_rn((double)(src - (N - 1)), dt), __dmul_rn(alpha, dt));
+                v = __dadd_rn(pv[(N - 1) * 2 + c], __dmul_rn(vel, extra));
+            }
+            L.prev[lane][c] = v;
+        }
+    } else if (lane < N) {
+        L.prev[lane][0] = 0.0;
+        L.prev[lane][1] = 0.0;
+    }
+    __syncthreads();
+    const bool cons = prev_ok && in.consistency_on && in.consistency_on[(size_t)sc * G + g] && pr.i_cons_w >= 0;
+
+    // ---- stream out the parameter block [N][npar]
+    const double* base = in.stage_params + (size_t)sc * npar;
+    double* P = params + (size_t)sol * N * npar;
+    const int lin0 = pr.i_lin0, ell0 = pr.i_ell0;
+    for (int e = lane; e < N * npar; e += 64) {
+        const int k = e / npar, idx = e - k * npar;
+        double v = base[idx];
+        if (NL > 0 && idx >= lin0 && idx < lin0 + 3 * NL) {
+            const int i = (idx - lin0) / 3, c = (idx - lin0) - 3 * i;
+            if (guided && k >= 1 && i < n_obs) v = L.lin[k][i][c];
+            else v = c == 0 ? 1.0 : (c == 1 ? 0.0 : __dadd_rn(x0, 100.0));
+        } else if (NE > 0 && idx >= ell0 && idx < ell0 + 7 * NE) {
+            const int j = (idx - ell0) / 7, c = (idx - ell0) - 7 * j;
+            if (k == 0) {
+                const double dummy[7] = {__dadd_rn(x0, 50.0), __dadd_rn(y0, 50.0), 0.0, 0.0, 0.0, 1.0, 0.1};
+                v = dummy[c];
+            } else {
+                const double* o = in.obst + (((size_t)sc * NE + j) * N + (k - 1)) * 5;
+                const double* m = in.obst_meta + ((size_t)sc * NE + j) * 2;
+                v = c < 5 ? o[c] : (c == 5 ? m[1] : m[0]);  // x y psi major minor | chi r
+            }
+        } else if (pr.i_cons_w >= 0 && (idx == pr.i_cons_w || idx == pr.i_prev_x || idx == pr.i_prev_y)) {
+            const bool on = cons && k >= 1 && k <= N - 2;
+            v = !on ? 0.0 : (idx == pr.i_cons_w ? in.w_consistency : L.prev[k][idx == pr.i_prev_x ? 0 : 1]);
+        }
+        P[e] = v;
+    }
+    double* W = warm + (size_t)sol * (N + 1) * MPCG_NVAR;
+    for (int e = lane; e < (N + 1) * MPCG_NVAR; e += 64) W[e] = (&L.warm[0][0])[e];
+    if (lane < MPCG_NX) xinit[(size_t)sol * MPCG_NX + lane] = st[lane];
+    if (g == 0 && prev_out && lane < N) {
+        prev_out[((size_t)sc * N + lane) * 2 + 0] = L.prev[lane][0];
+        prev_out[((size_t)sc * N + lane) * 2 + 1] = L.prev[lane][1];
+    }
+    if (cons_active && lane == 0) cons_active[sol] = cons ? 1 : 0;
+}
+
+}  // namespace mpcg

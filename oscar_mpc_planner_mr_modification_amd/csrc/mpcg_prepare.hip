@@ -1,0 +1,42 @@
+// mpcg_prepare.hip — entry point of the per-guess input producers
+// (mpcg_prepare, include/mpcg.h).  Compiled on its own with
+// -ffp-contract=off: the producers must agree bit for bit with the host
+// restatement (producers.py), so no multiply-add may be fused here, while the
+// solve kernels in mpcg_kernels.hip keep contraction on.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "mpcg.h"
+#include "mpcg_prepare.h"
+
+namespace mpcg {
+extern thread_local std::string g_err;  // defined in mpcg_kernels.hip
+}
+
+extern "C" {
+
+int mpcg_prepare(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg_scene_io* in, double* params,
+                 double* warm, double* xinit, double* prev_interp, unsigned char* consistency_active, void* stream) {
+    if (!pr || !in || n_scenes < 0 || n_guesses < 1 || !params || !warm || !xinit || !in->stage_params ||
+        !in->state || (pr->n_ell > 0 && (!in->obst || !in->obst_meta)) || !in->guidance) {
+        mpcg::g_err = "mpcg_prepare: invalid arguments";
+        return -1;
+    }
+    const int n_obs = pr->n_lin < pr->n_ell ? pr->n_lin : pr->n_ell;
+    if (pr->N > mpcg::PREP_MAX_N || n_obs > mpcg::PREP_MAX_OBS || pr->N < 2) {
+        mpcg::g_err = "mpcg_prepare: N or the obstacle count exceeds the kernel's limits";
+        return -2;
+    }
+    if (n_scenes == 0) return 0;
+    hipLaunchKernelGGL(mpcg::prepare_kernel, dim3(n_scenes * n_guesses), dim3(64), 0, (hipStream_t)stream, *pr,
+                       n_scenes, n_guesses, *in, params, warm, xinit, prev_interp, consistency_active);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        mpcg::g_err = std::string("prepare launch: ") + hipGetErrorString(e);
+        return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"

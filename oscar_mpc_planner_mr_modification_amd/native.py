@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX,  # noqa: F401
-                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, problem_from_layout)
+                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, problem_from_layout)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 # MPCG_LIB selects a diagnostic build (e.g. libmpcg_stamps.so); default the production library
@@ -53,6 +53,8 @@ def _load():
     lib.mpcg_select_best_device.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, C.c_double, vp, vp,
                                             C.c_double, vp, vp, vp, vp]
     lib.mpcg_select_best_device.restype = C.c_int
+    lib.mpcg_prepare.argtypes = [P, C.c_int, C.c_int, C.POINTER(MpcgSceneIo), vp, vp, vp, vp, vp, vp]
+    lib.mpcg_prepare.restype = C.c_int
     if lib.mpcg_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
@@ -194,3 +196,47 @@ def select_best_device(n_scenes, n_guesses, N, xtraj, pobj, exit_code, prev_traj
                                      _ptr(best), _ptr(objective), C.c_void_p(s.cuda_stream))
     _check(rc, "mpcg_select_best_device")
     return best, objective
+
+
+def scenes_to_device(scenes, device):
+    """producers.Scenes -> dict of contiguous device tensors (float64 / uint8)."""
+    import torch
+
+    def t(a, dt=torch.float64):
+        return None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
+
+    return dict(stage_params=t(scenes.stage_params), state=t(scenes.state), obst=t(scenes.obst),
+                obst_meta=t(scenes.obst_meta), guidance=t(scenes.guidance),
+                guided=t(scenes.guided.astype(np.uint8), torch.uint8), main_warm=t(scenes.main_warm),
+                prev_traj=t(scenes.prev_traj), prev_elapsed=t(scenes.prev_elapsed),
+                consistency_on=t(scenes.consistency_on.astype(np.uint8), torch.uint8),
+                previously_selected=t(scenes.previously_selected.astype(np.uint8), torch.uint8),
+                n_scenes=scenes.n_scenes, n_guesses=scenes.n_guesses)
+
+
+def prepare_device(pr: MpcgProblem, dsc: dict, robot_radius: float, w_consistency: float, deceleration: float = 3.0,
+                   out=None, stream=None):
+    """mpcg_prepare: per-planner solver inputs from device-resident scene data
+    (`scenes_to_device`).  Returns dict(params, warm, xinit, prev_interp,
+    consistency_active) of device tensors; asynchronous on `stream`."""
+    import torch
+
+    S, G, N = dsc["n_scenes"], dsc["n_guesses"], pr.N
+    dev = dsc["state"].device
+    assert tuple(dsc["stage_params"].shape) == (S, pr.npar)
+    assert tuple(dsc["obst"].shape) == (S, pr.n_ell, N, 5) and tuple(dsc["guidance"].shape) == (S, G, N + 1, 4)
+    if out is None:
+        out = dict(params=torch.empty((S * G, N, pr.npar), dtype=torch.float64, device=dev),
+                   warm=torch.empty((S * G, N + 1, NVAR), dtype=torch.float64, device=dev),
+                   xinit=torch.empty((S * G, NX), dtype=torch.float64, device=dev),
+                   prev_interp=torch.empty((S, N, 2), dtype=torch.float64, device=dev),
+                   consistency_active=torch.empty((S * G,), dtype=torch.uint8, device=dev))
+    p = lambda k: None if dsc.get(k) is None else dsc[k].data_ptr()  # noqa: E731
+    sio = MpcgSceneIo(p("stage_params"), p("state"), p("obst"), p("obst_meta"), p("guidance"), p("guided"),
+                      p("main_warm"), p("prev_traj"), p("prev_elapsed"), p("consistency_on"),
+                      float(robot_radius), float(w_consistency), float(deceleration))
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    rc = lib.mpcg_prepare(C.byref(pr), S, G, C.byref(sio), _ptr(out["params"]), _ptr(out["warm"]), _ptr(out["xinit"]),
+                          _ptr(out["prev_interp"]), _ptr(out["consistency_active"]), C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_prepare")
+    return out

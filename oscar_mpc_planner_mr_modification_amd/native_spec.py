@@ -73,9 +73,18 @@ class MpcgIo(C.Structure):
                 ("exit_code", C.c_void_p), ("info", C.c_void_p), ("lam_out", C.c_void_p)]
 
 
+class MpcgSceneIo(C.Structure):
+    """Mirror of `mpcg_scene_io` (include/mpcg.h)."""
+    _fields_ = [("stage_params", C.c_void_p), ("state", C.c_void_p), ("obst", C.c_void_p),
+                ("obst_meta", C.c_void_p), ("guidance", C.c_void_p), ("guided", C.c_void_p),
+                ("main_warm", C.c_void_p), ("prev_traj", C.c_void_p), ("prev_elapsed", C.c_void_p),
+                ("consistency_on", C.c_void_p), ("robot_radius", C.c_double), ("w_consistency", C.c_double),
+                ("deceleration", C.c_double)]
+
+
 ABI_VERSION = 2
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
            "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
-           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device")
+           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare")
 
 

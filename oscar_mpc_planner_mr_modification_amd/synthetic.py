@@ -2,18 +2,23 @@
 
 One scene = one control step of `Planner::solveMPC` on the jackal T-MPC
 problem: a 5-segment reference path, the ego state, `n_obs` constant-velocity
-obstacles and G = n_guided + 1 planners (the guided ones plus the T-MPC++
-non-guided one).  For every (scene, planner) pair this module writes exactly
-what the reference's host-side modules write before `Solver::solve()`:
+obstacles (padded to max_obstacles with the planner's far-away dummies), the
+previous plan, and G = n_guided + 1 planners (the guided ones plus the T-MPC++
+non-guided one) with their guidance trajectories.  `make_scenes` returns the
+scene-level data (producers.Scenes); `make_batch` turns it into per-planner
+solver inputs with producers.prepare_host, i.e. exactly what the reference's
+host-side modules write before `Solver::solve()`:
 
 * weights + spline segments for every stage      (mpc_base.cpp:23-35, contouring.cpp:52-126)
-* topology halfspaces from the guess trajectory    (linearized_constraints.cpp:49-128, 150-189;
-  radius 1e-3 + robot_radius because `_use_guidance`, robot centre, no disc;
-  the Douglas-Rachford projection (:130-148, external ros_tools) is omitted)
+* topology halfspaces from the guess trajectory    (linearized_constraints.cpp:49-189;
+  radius 1e-3 + robot_radius because `_use_guidance`, robot centre, no disc,
+  Douglas-Rachford projection to safety first)
 * stage-0 dummies                                   (linearized_constraints.cpp:155-166,
                                                      ellipsoid_constraints.cpp:42-56)
 * obstacle ellipsoids, stage k uses prediction k-1 (ellipsoid_constraints.cpp:61-86)
-* consistency parameters on stages 1..N-2           (guidance_constraints.cpp:986-1023)
+* consistency parameters on stages 1..N-2 of the planners whose topology
+  was selected last step, from the previous plan interpolated by the elapsed
+  time                                              (guidance_constraints.cpp:951-1133)
 * warm start: braking for the non-guided planner    (acados_solver_interface.cpp:303-342)
   and guidance-initialised x, y, psi, v on k=1..N-1 for the guided ones
   (guidance_constraints.cpp:546-570), a/w/spline from the braking warm start.
@@ -29,6 +34,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from .layouts import Layout
+from .producers import Scenes, prepare_host
 
 SETTINGS_WEIGHTS = {  # mpc_planner_jackalsimulator/config/settings.yaml:78-92
     "acceleration": 0.34, "angular_velocity": 0.85, "velocity": 0.55,
@@ -38,6 +44,7 @@ SETTINGS_WEIGHTS = {  # mpc_planner_jackalsimulator/config/settings.yaml:78-92
 ROBOT_RADIUS = 0.325          # settings.yaml:38
 OBSTACLE_RADIUS = 0.325       # settings.yaml:43
 DECELERATION = 3.0            # settings.yaml:36 deceleration_at_infeasible
+CONTROL_PERIOD = 0.05         # settings.yaml:8 control_frequency 20 Hz
 SEED0 = 20251212
 
 
@@ -51,6 +58,9 @@ class Batch:
     n_scenes: int
     n_guesses: int
     prev_traj: np.ndarray  # (B, N, 2) interpolated previous trajectory (consistency reference)
+    consistency_on: np.ndarray = None       # (B*G,) bool, planners with the consistency cost
+    previously_selected: np.ndarray = None  # (B*G,) bool, guidance selected in the previous step
+    scenes: Scenes = None
 
 
 def _path(rng, n_seg):
@@ -162,39 +172,28 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
     return traj[idx], vel[idx]
 
 
-def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
-               seed: int = SEED0, first_scene: int = 0, consistency: bool = True, workers: int = 1) -> Batch:
-    """Scenes [first_scene, first_scene + n_scenes) x n_guesses planners.  With
-    workers > 1 the scenes are generated in a process pool; per-scene seeding
-    makes the result identical to the serial one."""
-    if workers > 1 and n_scenes >= 2 * workers:
-        from concurrent.futures import ProcessPoolExecutor
-
-        chunks = np.array_split(np.arange(n_scenes), workers)
-        with ProcessPoolExecutor(max_workers=workers) as ex:
-            futs = [ex.submit(_make_batch_serial, layout, len(c), n_guesses, n_obs, seed, first_scene + int(c[0]),
-                              consistency) for c in chunks if len(c)]
-            parts = [f.result() for f in futs]
-        return Batch(params=np.concatenate([p.params for p in parts]), warm=np.concatenate([p.warm for p in parts]),
-                     xinit=np.concatenate([p.xinit for p in parts]), guided=np.concatenate([p.guided for p in parts]),
-                     n_scenes=n_scenes, n_guesses=n_guesses, prev_traj=np.concatenate([p.prev_traj for p in parts]))
-    return _make_batch_serial(layout, n_scenes, n_guesses, n_obs, seed, first_scene, consistency)
-
-
-def _make_batch_serial(layout: Layout, n_scenes: int, n_guesses: int, n_obs: int | None,
-                       seed: int, first_scene: int, consistency: bool) -> Batch:
-    N, npar, dt = layout.N, layout.npar, layout.dt
-    n_obs = layout.max_obstacles if n_obs is None else n_obs
-    assert n_obs <= layout.max_obstacles
+def make_scenes(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
+                seed: int = SEED0, first_scene: int = 0) -> Scenes:
+    """Scene-level inputs (producers.Scenes) of scenes [first_scene, first_scene + n_scenes)."""
+    N, dt = layout.N, layout.dt
+    npar, ix = layout.npar, layout.idx
+    ne = layout.n_ell
+    n_obs = ne if n_obs is None else n_obs
+    assert n_obs <= ne
     G = n_guesses
-    S = n_scenes * G
-    params = np.zeros((S, N, npar))
-    warm = np.zeros((S, N + 1, 7))
-    xinit = np.zeros((S, 5))
-    guided = np.zeros(S, bool)
-    prev = np.zeros((n_scenes, N, 2))
-    ix = layout.idx
-    for sc in range(n_scenes):
+    S = n_scenes
+    stage_params = np.zeros((S, npar))
+    state = np.zeros((S, 5))
+    obst = np.zeros((S, ne, N, 5))
+    meta = np.zeros((S, ne, 2))
+    guidance = np.zeros((S, G, N + 1, 4))
+    guided = np.zeros((S, G), bool)
+    guided[:, :G - 1] = True
+    prev = np.zeros((S, N, 2))
+    elapsed = np.full(S, np.nan)
+    cons_on = np.zeros((S, G), bool)
+    prev_sel = np.zeros((S, G), bool)
+    for sc in range(S):
         rng = np.random.default_rng(seed + first_scene + sc)
         coef, starts = _path(rng, layout.n_seg)
         s_ego = rng.uniform(0.0, 1.0)
@@ -204,6 +203,7 @@ def _make_batch_serial(layout: Layout, n_scenes: int, n_guesses: int, n_obs: int
         v0 = rng.uniform(0.0, 2.0)
         psi0 = np.arctan2(t_on[1], t_on[0]) + rng.normal(0.0, 0.1)
         x0 = np.array([ego_pos[0], ego_pos[1], psi0, v0, s_ego])
+        state[sc] = x0
         obstacles = []
         for j in range(n_obs):
             ahead = rng.uniform(2.0, 10.0)
@@ -211,13 +211,12 @@ def _make_batch_serial(layout: Layout, n_scenes: int, n_guesses: int, n_obs: int
             pj, tj = _path_eval(coef, starts, s_ego + ahead)
             nj = np.array([-tj[1], tj[0]])
             obstacles.append((pj + lat * nj, rng.normal(0.0, 0.7, size=2)))
-        # scene-shared parameters (identical for every planner and stage)
-        base = np.zeros(npar)
-        for name, key in (("acceleration", "acceleration"), ("angular_velocity", "angular_velocity"),
-                          ("velocity", "velocity"), ("reference_velocity", "reference_velocity"),
-                          ("contour", "contour"), ("lag", "lag"), ("terminal_angle", "terminal_angle"),
-                          ("terminal_contouring", "terminal_contouring")):
-            base[ix(name)] = SETTINGS_WEIGHTS[key]
+        # stage-invariant module parameters (mpc_base.cpp:23-35, contouring.cpp:52-126,
+        # ellipsoid_constraints.cpp:38-40)
+        base = stage_params[sc]
+        for name in ("acceleration", "angular_velocity", "velocity", "reference_velocity", "contour", "lag",
+                     "terminal_angle", "terminal_contouring"):
+            base[ix(name)] = SETTINGS_WEIGHTS[name]
         for j in range(layout.n_seg):
             for ax, axn in enumerate("xy"):
                 for ci, cn in enumerate("abcd"):
@@ -225,67 +224,69 @@ def _make_batch_serial(layout: Layout, n_scenes: int, n_guesses: int, n_obs: int
             base[ix(f"spline{j}_start")] = starts[j]
         base[ix("ego_disc_radius")] = ROBOT_RADIUS
         base[ix("ego_disc_0_offset")] = 0.0
-        stage = np.repeat(base[None, :], N, 0)
-        # ellipsoids: stage 0 dummies, stage k>=1 prediction k-1 (deterministic)
-        for j in range(layout.n_ell):
-            b0 = ix(f"ellipsoid_obst_{j}_x")
-            stage[0, b0:b0 + 7] = (x0[0] + 50.0, x0[1] + 50.0, 0.0, 0.0, 0.0, 1.0, 0.1)
+        # obstacles: constant-velocity deterministic predictions (data_preparation.cpp:60-81),
+        # padded with dummies at (x + 100, y + 100), radius 0
+        for j in range(ne):
             if j < n_obs:
                 op, ov = obstacles[j]
-                kk = np.arange(N - 1)[:, None]
-                stage[1:, b0:b0 + 2] = op[None, :] + ov[None, :] * dt * kk
-                stage[1:, b0 + 2:b0 + 7] = (0.0, 0.0, 0.0, 1.0, OBSTACLE_RADIUS)
-            else:  # ensureObstacleSize pads with far-away dummies (data_preparation.cpp:49-55)
-                stage[1:, b0:b0 + 7] = (x0[0] + 100.0, x0[1] + 100.0, 0.0, 0.0, 0.0, 1.0, 0.0)
-        # consistency reference: the previous plan, i.e. a constant-speed
-        # roll-out along the initial heading (guidance_constraints.cpp:1073-1133)
-        vp = max(v0, 0.5)
-        for k in range(N):
-            prev[sc, k] = ego_pos + vp * dt * k * np.array([np.cos(psi0), np.sin(psi0)])
-        if layout.consistency:
-            wcons = SETTINGS_WEIGHTS["consistency"] if consistency else 0.0
+                obst[sc, j, :, 0:2] = op[None, :] + ov[None, :] * dt * np.arange(N)[:, None]
+                meta[sc, j] = (OBSTACLE_RADIUS, 1.0)
+            else:
+                obst[sc, j, :, 0:2] = (x0[0] + 100.0, x0[1] + 100.0)
+                meta[sc, j] = (0.0, 1.0)
+        # previous plan stored one control period ago: a constant-speed roll-out
+        # along the heading; one scene in ten is a first step without one
+        if rng.uniform() >= 0.1:
+            vp = max(v0, 0.5)
+            dirv = np.array([np.cos(psi0), np.sin(psi0)])
             for k in range(N):
-                valid = 1 <= k <= N - 2
-                stage[k, ix("consistency_weight")] = wcons if valid else 0.0
-                stage[k, ix("prev_traj_x")] = prev[sc, k, 0] if valid else 0.0
-                stage[k, ix("prev_traj_y")] = prev[sc, k, 1] if valid else 0.0
-        brake = _braking(x0.copy(), N, dt)
-        # obs_pred[k, i] = prediction k-1 of obstacle i (stage k >= 1)
-        obs_pred = np.zeros((N, n_obs, 2))
-        for i, (op, ov) in enumerate(obstacles):
-            obs_pred[1:, i] = op[None, :] + ov[None, :] * dt * np.arange(N - 1)[:, None]
-        for g in range(G):
-            sidx = sc * G + g
-            P = stage.copy()
-            is_guided = g < G - 1
-            w = brake.copy()
-            lin = ix("lin_constraint_0_a1")
-            # dummies everywhere first (a1=1, a2=0, b=x+100: linearized_constraints.h:28, .cpp:54)
-            for i in range(layout.n_lin):
-                P[:, lin + 3 * i:lin + 3 * i + 3] = (1.0, 0.0, x0[0] + 100.0)
-            if is_guided:
-                signs = [1 if (g >> (j % 3)) & 1 else -1 for j in range(n_obs)]
-                if g >= 8:
-                    signs = list(np.random.default_rng(seed + 7919 * sidx).choice([-1, 1], n_obs))
-                pos, vel = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
-                                             SETTINGS_WEIGHTS["reference_velocity"])
-                w[1:N, 2:4] = pos[1:N]
-                w[1:N, 4] = np.arctan2(vel[1:N, 1], vel[1:N, 0])
-                w[1:N, 5] = np.hypot(vel[1:N, 0], vel[1:N, 1])
-                if n_obs:
-                    # LinearizedConstraints::update (linearized_constraints.cpp:84-105)
-                    ob = obs_pred[1:N]                                # (N-1, n_obs, 2)
-                    dxy = ob - pos[1:N, None, :]
-                    dist = np.hypot(dxy[..., 0], dxy[..., 1])
-                    a1 = dxy[..., 0] / dist
-                    a2 = dxy[..., 1] / dist
-                    bb = a1 * ob[..., 0] + a2 * ob[..., 1] - (1e-3 + ROBOT_RADIUS)
-                    blk = P[1:N, lin:lin + 3 * n_obs].reshape(N - 1, n_obs, 3)
-                    blk[..., 0], blk[..., 1], blk[..., 2] = a1, a2, bb
-                    P[1:N, lin:lin + 3 * n_obs] = blk.reshape(N - 1, 3 * n_obs)
-            params[sidx] = P
-            warm[sidx] = w
-            xinit[sidx] = x0
-            guided[sidx] = is_guided
-    return Batch(params=params, warm=warm, xinit=xinit, guided=guided, n_scenes=n_scenes,
-                 n_guesses=G, prev_traj=prev)
+                prev[sc, k] = ego_pos + vp * (k * dt - CONTROL_PERIOD) * dirv
+            elapsed[sc] = CONTROL_PERIOD
+            sel = int(rng.integers(0, G))
+            if sel == G - 1:
+                cons_on[sc, G - 1] = True       # consistency_on_non_guided_planner: true (settings.yaml)
+            else:
+                cons_on[sc, sel] = True         # the guided planner of the selected topology
+                prev_sel[sc, sel] = True
+        for g in range(G - 1):
+            signs = [1 if (g >> (j % 3)) & 1 else -1 for j in range(n_obs)]
+            if g >= 8:
+                signs = list(np.random.default_rng(seed + 7919 * ((first_scene + sc) * G + g)).choice([-1, 1], n_obs))
+            pos, vel = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
+                                         SETTINGS_WEIGHTS["reference_velocity"])
+            guidance[sc, g, :, 0:2] = pos
+            guidance[sc, g, :, 2:4] = vel
+    return Scenes(stage_params=stage_params, state=state, obst=obst, obst_meta=meta, guidance=guidance,
+                  guided=guided, prev_traj=prev, prev_elapsed=elapsed, consistency_on=cons_on,
+                  previously_selected=prev_sel, main_warm=None)
+
+
+def concat_scenes(parts) -> Scenes:
+    return Scenes(**{f: np.concatenate([getattr(p, f) for p in parts]) for f in
+                     ("stage_params", "state", "obst", "obst_meta", "guidance", "guided", "prev_traj",
+                      "prev_elapsed", "consistency_on", "previously_selected")}, main_warm=None)
+
+
+def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
+               seed: int = SEED0, first_scene: int = 0, consistency: bool = True, workers: int = 1) -> Batch:
+    """Scenes [first_scene, first_scene + n_scenes) x n_guesses planners, as
+    per-planner solver inputs.  With workers > 1 the scenes are generated in a
+    process pool; per-scene seeding makes the result identical to the serial one."""
+    if workers > 1 and n_scenes >= 2 * workers:
+        from concurrent.futures import ProcessPoolExecutor
+
+        chunks = np.array_split(np.arange(n_scenes), workers)
+        with ProcessPoolExecutor(max_workers=workers) as ex:
+            futs = [ex.submit(make_scenes, layout, len(c), n_guesses, n_obs, seed, first_scene + int(c[0]))
+                    for c in chunks if len(c)]
+            sc = concat_scenes([f.result() for f in futs])
+    else:
+        sc = make_scenes(layout, n_scenes, n_guesses, n_obs, seed, first_scene)
+    if not consistency:
+        sc.consistency_on[:] = False
+    p = prepare_host(layout, sc, ROBOT_RADIUS, SETTINGS_WEIGHTS["consistency"], DECELERATION)
+    G = n_guesses
+    return Batch(params=p.params, warm=p.warm, xinit=p.xinit, guided=sc.guided.reshape(-1), n_scenes=n_scenes,
+                 n_guesses=G, prev_traj=p.prev_interp,
+                 consistency_on=(sc.consistency_on & p.prev_valid[:, None]).reshape(-1),
+                 previously_selected=sc.previously_selected.reshape(-1), scenes=sc)

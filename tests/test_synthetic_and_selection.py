@@ -33,9 +33,12 @@ def test_reference_parameter_semantics(lay):
         np.testing.assert_allclose(P[0, j0:j0 + 7], [x0[0] + 50, x0[1] + 50, 0, 0, 0, 1, 0.1])
         l0 = ix("lin_constraint_0_a1")
         np.testing.assert_allclose(P[0, l0:l0 + 3], [1.0, 0.0, x0[0] + 100])
-        # consistency only on stages 1..N-2 (guidance_constraints.cpp:1009-1011)
+        # consistency only on stages 1..N-2 of the planners that carry it (guidance_constraints.cpp:1009-1011)
         w = P[:, ix("consistency_weight")]
-        assert w[0] == 0 and w[N - 1] == 0 and (w[1:N - 1] == 0.05).all()
+        if b.consistency_on[s]:
+            assert w[0] == 0 and w[N - 1] == 0 and (w[1:N - 1] == 0.05).all()
+        else:
+            assert (w == 0).all()
         # weights identical on every stage
         assert (P[:, ix("lag")] == 0.75).all() and (P[:, ix("velocity")] == 0.55).all()
         # stage k uses obstacle prediction k-1: constant velocity steps of dt
