@@ -152,6 +152,43 @@ int mpcg_prepare(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg
                  double *params, double *warm, double *xinit, double *prev_interp,
                  unsigned char *consistency_active, void *stream);
 
+/* Bookkeeping between two control steps of every scene: the state the
+ * reference keeps in Planner / GuidanceConstraints / each LocalPlanner's
+ * solver (device pointers; semantics restated in producers.advance_host).
+ * Inputs (step t):
+ *   best [S]                        FindBestPlanner result, -1 = no feasible planner
+ *   exit_code [S*G], xtraj, utraj   the solves of step t
+ *   warm [S*G][N+1][nvar]           the warm start each planner used (its x0)
+ *   lam_out [S*G][N][nx+nh]         multipliers after the solves, or NULL
+ *   state_next [S][nx]              ego state at step t+1
+ *   guided [S][G]                   planner kinds (the non-guided one is the "original planner")
+ *   topology, topology_next [S][G]  topology class of every planner at t and t+1, or NULL = planner index
+ *   previously_selected [S][G]      selection flags at t (kept when no planner was feasible), or NULL
+ * Outputs (step t+1):
+ *   main_warm_next [S][N+1][nvar]   Planner::solveMPC: initializeWarmstart(state, shift) of the
+ *                                   winner's output (x0[N] from the winner's parameters) when step t
+ *                                   was feasible, else the braking plan (planner.cpp:129-137)
+ *   prev_traj_next [S][N][2], prev_elapsed_next [S]  storePreviousTrajectoryFromSolver (NaN: none)
+ *   consistency_on_next [S][G]      shouldEnableConsistencyForPlanner (guidance_constraints.cpp:951-984)
+ *   previously_selected_next [S][G] OverrideSelectedTrajectory (:500-513)
+ *   lam_next [S*G][N][nx+nh]        each planner's carried multipliers, zeroed after a failed solve */
+typedef struct mpcg_step_io {
+    const int *best, *exit_code;
+    const double *xtraj, *utraj, *warm, *lam_out, *state_next;
+    const unsigned char *guided;
+    const int *topology, *topology_next;
+    const unsigned char *previously_selected;
+    int shift_forward;              /* shift_previous_solution_forward && enable_output */
+    int consistency_on_non_guided;  /* JULES.consistency_on_non_guided_planner */
+    double elapsed;                 /* seconds from step t to step t+1 */
+    double deceleration;            /* deceleration_at_infeasible */
+} mpcg_step_io;
+
+int mpcg_advance(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg_step_io *io,
+                 double *main_warm_next, double *prev_traj_next, double *prev_elapsed_next,
+                 unsigned char *consistency_on_next, unsigned char *previously_selected_next, double *lam_next,
+                 void *stream);
+
 /* 0 if (N, n_lin, n_ell) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);
 

@@ -220,3 +220,99 @@ __global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scen
 }
 
 }  // namespace mpcg
+
+namespace mpcg {
+
+// Between two control steps (include/mpcg.h, mpcg_advance); one workgroup per scene.
+__global__ __launch_bounds__(64) void advance_kernel(mpcg_problem pr, int n_scenes, int G, mpcg_step_io io,
+                                                     double* __restrict__ main_warm, double* __restrict__ prev_traj,
+                                                     double* __restrict__ prev_elapsed,
+                                                     unsigned char* __restrict__ cons_on,
+                                                     unsigned char* __restrict__ prev_sel,
+                                                     double* __restrict__ lam_next) {
+    const int sc = blockIdx.x;
+    if (sc >= n_scenes) return;
+    const int lane = threadIdx.x;
+    const int N = pr.N, NV = MPCG_NVAR, NXs = MPCG_NX, NUs = MPCG_NU;
+    const double dt = pr.dt;
+    const int best = io.best[sc];
+    const bool feasible = best >= 0;
+    const int b = sc * G + (feasible ? best : 0);
+    const double* st = io.state_next + (size_t)sc * NXs;
+    double* W = main_warm + (size_t)sc * (N + 1) * NV;
+    if (feasible) {
+        const double* xt = io.xtraj + (size_t)b * (N + 1) * NXs;
+        const double* ut = io.utraj + (size_t)b * N * NUs;
+        const double* wb = io.warm + (size_t)b * (N + 1) * NV;
+        for (int e = lane; e < (N + 1) * NV; e += 64) {
+            const int k = e / NV, i = e - k * NV;
+            double v;
+            if (!io.shift_forward) {
+                // [x_0 .. x_{N-1}] of the winner; x0[N] stays the winner's own warm start
+                v = k < N ? (i < NUs ? ut[k * NUs + i] : xt[k * NXs + i - NUs]) : wb[N * NV + i];
+            } else {
+                // [state, out_2, ..., out_{N-1}, out_{N-1}, out_{N-1}] (acados_solver_interface.cpp:346-368);
+                // the reference reads the inputs of stage 0 out of State's range: here out_1's inputs
+                const int src = k == 0 ? 1 : (k >= N - 1 ? N - 1 : k + 1);
+                v = i < NUs ? ut[src * NUs + i] : (k == 0 ? st[i - NUs] : xt[src * NXs + i - NUs]);
+            }
+            W[e] = v;
+        }
+        if (lane < N) {
+            prev_traj[((size_t)sc * N + lane) * 2 + 0] = xt[lane * NXs + 0];
+            prev_traj[((size_t)sc * N + lane) * 2 + 1] = xt[lane * NXs + 1];
+        }
+    } else {
+        if (lane == 0) {
+            // Solver::initializeWithBraking(state)
+            double x = st[0], y = st[1], psi = st[2], v = st[3], s = st[4];
+            const double a = -fabs(io.deceleration);
+            const double c = cos(psi), sn = sin(psi);
+            for (int k = 0; k <= N; ++k) {
+                if (k > 0) {
+                    x = __dadd_rn(x, __dmul_rn(__dmul_rn(v, dt), c));
+                    y = __dadd_rn(y, __dmul_rn(__dmul_rn(v, dt), sn));
+                    s = __dadd_rn(s, __dmul_rn(v, dt));
+                    v = fmax(__dadd_rn(v, __dmul_rn(a, dt)), 0.0);
+                }
+                double* w = W + k * NV;
+                w[0] = a; w[1] = 0.0; w[2] = x; w[3] = y; w[4] = psi; w[5] = v; w[6] = s;
+            }
+        }
+        if (lane < N) {
+            prev_traj[((size_t)sc * N + lane) * 2 + 0] = 0.0;
+            prev_traj[((size_t)sc * N + lane) * 2 + 1] = 0.0;
+        }
+    }
+    if (lane == 0) prev_elapsed[sc] = feasible ? io.elapsed : __longlong_as_double(0x7ff8000000000000LL);
+    // consistency / selection flags of the next step
+    const bool best_original = feasible && !(io.guided && io.guided[(size_t)sc * G + best]);
+    const int sel_topo = feasible ? (io.topology ? io.topology[(size_t)sc * G + best] : best) : -1;
+    for (int g = lane; g < G; g += 64) {
+        const size_t i = (size_t)sc * G + g;
+        const bool guided = io.guided && io.guided[i];
+        const int topo = io.topology_next ? io.topology_next[i] : g;
+        bool on = false, ps;
+        if (feasible) {
+            on = guided ? (!best_original && topo == sel_topo) : (io.consistency_on_non_guided && best_original);
+            ps = guided && !best_original && topo == sel_topo;
+        } else {
+            ps = io.previously_selected ? io.previously_selected[i] != 0 : false;
+        }
+        cons_on[i] = on ? 1 : 0;
+        prev_sel[i] = ps ? 1 : 0;
+    }
+    // carried multipliers of every planner (Solver_acados_reset zeroes them after a failure)
+    if (lam_next) {
+        const int L = N * (NXs + pr.n_lin + pr.n_ell);
+        for (int g = 0; g < G; ++g) {
+            const size_t i = (size_t)sc * G + g;
+            const bool ok = io.exit_code[i] == 1 && io.lam_out;
+            double* dst = lam_next + i * L;
+            const double* src = ok ? io.lam_out + i * L : nullptr;
+            for (int e = lane; e < L; e += 64) dst[e] = ok ? src[e] : 0.0;
+        }
+    }
+}
+
+}  // namespace mpcg

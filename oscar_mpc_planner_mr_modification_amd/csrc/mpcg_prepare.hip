@@ -39,4 +39,25 @@ int mpcg_prepare(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg
     return 0;
 }
 
+int mpcg_advance(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg_step_io* io, double* main_warm_next,
+                 double* prev_traj_next, double* prev_elapsed_next, unsigned char* consistency_on_next,
+                 unsigned char* previously_selected_next, double* lam_next, void* stream) {
+    if (!pr || !io || n_scenes < 0 || n_guesses < 1 || !io->best || !io->exit_code || !io->xtraj || !io->utraj ||
+        !io->warm || !io->state_next || !main_warm_next || !prev_traj_next || !prev_elapsed_next ||
+        !consistency_on_next || !previously_selected_next) {
+        mpcg::g_err = "mpcg_advance: invalid arguments";
+        return -1;
+    }
+    if (n_scenes == 0) return 0;
+    hipLaunchKernelGGL(mpcg::advance_kernel, dim3(n_scenes), dim3(64), 0, (hipStream_t)stream, *pr, n_scenes,
+                       n_guesses, *io, main_warm_next, prev_traj_next, prev_elapsed_next, consistency_on_next,
+                       previously_selected_next, lam_next);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        mpcg::g_err = std::string("advance launch: ") + hipGetErrorString(e);
+        return -1;
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX,  # noqa: F401
-                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, problem_from_layout)
+                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, MpcgStepIo,
+                          problem_from_layout)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 # MPCG_LIB selects a diagnostic build (e.g. libmpcg_stamps.so); default the production library
@@ -55,6 +56,8 @@ def _load():
     lib.mpcg_select_best_device.restype = C.c_int
     lib.mpcg_prepare.argtypes = [P, C.c_int, C.c_int, C.POINTER(MpcgSceneIo), vp, vp, vp, vp, vp, vp]
     lib.mpcg_prepare.restype = C.c_int
+    lib.mpcg_advance.argtypes = [P, C.c_int, C.c_int, C.POINTER(MpcgStepIo), vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcg_advance.restype = C.c_int
     if lib.mpcg_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
@@ -239,4 +242,35 @@ def prepare_device(pr: MpcgProblem, dsc: dict, robot_radius: float, w_consistenc
     rc = lib.mpcg_prepare(C.byref(pr), S, G, C.byref(sio), _ptr(out["params"]), _ptr(out["warm"]), _ptr(out["xinit"]),
                           _ptr(out["prev_interp"]), _ptr(out["consistency_active"]), C.c_void_p(s.cuda_stream))
     _check(rc, "mpcg_prepare")
+    return out
+
+
+def advance_device(pr: MpcgProblem, S: int, G: int, best, exit_code, xtraj, utraj, warm, lam_out, state_next, guided,
+                   elapsed: float, deceleration: float = 3.0, shift_forward: bool = False,
+                   consistency_on_non_guided: bool = True, topology=None, topology_next=None,
+                   previously_selected=None, stream=None):
+    """mpcg_advance: the carried state of the next control step (device tensors)."""
+    import torch
+
+    dev = xtraj.device
+    N = pr.N
+    LS = NX + pr.n_lin + pr.n_ell
+    out = dict(main_warm=torch.empty((S, N + 1, NVAR), dtype=torch.float64, device=dev),
+               prev_traj=torch.empty((S, N, 2), dtype=torch.float64, device=dev),
+               prev_elapsed=torch.empty((S,), dtype=torch.float64, device=dev),
+               consistency_on=torch.empty((S, G), dtype=torch.uint8, device=dev),
+               previously_selected=torch.empty((S, G), dtype=torch.uint8, device=dev),
+               lam=None if lam_out is None else torch.empty((S * G, N, LS), dtype=torch.float64, device=dev))
+    best32 = best.to(torch.int32).contiguous()
+    sio = MpcgStepIo(best32.data_ptr(), exit_code.data_ptr(), xtraj.data_ptr(), utraj.data_ptr(), warm.data_ptr(),
+                     None if lam_out is None else lam_out.data_ptr(), state_next.data_ptr(), guided.data_ptr(),
+                     None if topology is None else topology.data_ptr(),
+                     None if topology_next is None else topology_next.data_ptr(),
+                     None if previously_selected is None else previously_selected.data_ptr(),
+                     int(shift_forward), int(consistency_on_non_guided), float(elapsed), float(deceleration))
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    rc = lib.mpcg_advance(C.byref(pr), S, G, C.byref(sio), _ptr(out["main_warm"]), _ptr(out["prev_traj"]),
+                          _ptr(out["prev_elapsed"]), _ptr(out["consistency_on"]), _ptr(out["previously_selected"]),
+                          _ptr(out["lam"]), C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_advance")
     return out

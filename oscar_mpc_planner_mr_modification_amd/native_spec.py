@@ -82,9 +82,18 @@ class MpcgSceneIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
+class MpcgStepIo(C.Structure):
+    """Mirror of `mpcg_step_io` (include/mpcg.h)."""
+    _fields_ = [("best", C.c_void_p), ("exit_code", C.c_void_p), ("xtraj", C.c_void_p), ("utraj", C.c_void_p),
+                ("warm", C.c_void_p), ("lam_out", C.c_void_p), ("state_next", C.c_void_p), ("guided", C.c_void_p),
+                ("topology", C.c_void_p), ("topology_next", C.c_void_p), ("previously_selected", C.c_void_p),
+                ("shift_forward", C.c_int), ("consistency_on_non_guided", C.c_int), ("elapsed", C.c_double),
+                ("deceleration", C.c_double)]
+
+
 ABI_VERSION = 2
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
            "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
-           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare")
+           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance")
 
 

@@ -240,3 +240,64 @@ def prepare_host(layout: Layout, sc: Scenes, robot_radius: float, w_consistency:
     xinit = np.repeat(sc.state[:, None], G, 1)
     return Prepared(params=params.reshape(S * G, N, npar), warm=warm.reshape(S * G, N + 1, 7),
                     xinit=xinit.reshape(S * G, 5), prev_interp=prev_i, prev_valid=valid)
+
+
+@dataclass
+class Carried:
+    """What one control step leaves for the next (mpcg_advance)."""
+    main_warm: np.ndarray           # (S, N+1, 7)
+    prev_traj: np.ndarray           # (S, N, 2)
+    prev_elapsed: np.ndarray        # (S,)
+    consistency_on: np.ndarray      # (S, G) bool
+    previously_selected: np.ndarray  # (S, G) bool
+    lam: Optional[np.ndarray]       # (S*G, N, nx + nh)
+
+
+def advance_host(layout: Layout, best, exit_code, xtraj, utraj, warm, lam_out, state_next, guided,
+                 elapsed: float, deceleration: float = 3.0, shift_forward: bool = False,
+                 consistency_on_non_guided: bool = True, topology=None, topology_next=None,
+                 previously_selected=None) -> Carried:
+    """Bookkeeping between two control steps (include/mpcg.h, mpcg_advance):
+    Planner::solveMPC warm start (planner.cpp:129-137, acados_solver_interface.cpp:344-376),
+    storePreviousTrajectoryFromSolver / the selection flags (guidance_constraints.cpp:429-537, 951-984)
+    and each planner's carried multipliers (reset after a failure, acados_solver_interface.cpp:186-190)."""
+    N = layout.N
+    S, G = guided.shape
+    best = np.asarray(best)
+    topo = np.tile(np.arange(G), (S, 1)) if topology is None else np.asarray(topology)
+    topo_n = np.tile(np.arange(G), (S, 1)) if topology_next is None else np.asarray(topology_next)
+    main = braking(state_next, N, layout.dt, deceleration)
+    prev = np.zeros((S, N, 2))
+    el = np.full(S, np.nan)
+    cons = np.zeros((S, G), bool)
+    psel = np.zeros((S, G), bool) if previously_selected is None else np.array(previously_selected, bool)
+    for s in range(S):
+        if best[s] < 0:
+            continue
+        b = s * G + int(best[s])
+        xt, ut = xtraj[b], utraj[b]
+        if not shift_forward:
+            main[s, :N, :2] = ut
+            main[s, :N, 2:] = xt[:N]
+            main[s, N] = warm[b, N]
+        else:
+            for k in range(N + 1):
+                src = 1 if k == 0 else (N - 1 if k >= N - 1 else k + 1)
+                main[s, k, :2] = ut[src]
+                main[s, k, 2:] = state_next[s] if k == 0 else xt[src]
+        prev[s] = xt[:N, :2]
+        el[s] = elapsed
+        original = not guided[s, best[s]]
+        sel_topo = topo[s, best[s]]
+        for g in range(G):
+            if guided[s, g]:
+                cons[s, g] = (not original) and topo_n[s, g] == sel_topo
+                psel[s, g] = (not original) and topo_n[s, g] == sel_topo
+            else:
+                cons[s, g] = consistency_on_non_guided and original
+                psel[s, g] = False
+    lam = None
+    if lam_out is not None:
+        lam = np.where((np.asarray(exit_code) == 1)[:, None, None], lam_out, 0.0)
+    return Carried(main_warm=main, prev_traj=prev, prev_elapsed=el, consistency_on=cons,
+                   previously_selected=psel, lam=lam)

@@ -290,3 +290,21 @@ def make_batch(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | N
                  n_guesses=G, prev_traj=p.prev_interp,
                  consistency_on=(sc.consistency_on & p.prev_valid[:, None]).reshape(-1),
                  previously_selected=sc.previously_selected.reshape(-1), scenes=sc)
+
+
+def step_scenes(layout: Layout, sc: Scenes, state_next: np.ndarray, carried) -> Scenes:
+    """The next control step of the synthetic scenes, one integrator step
+    (dt) later: obstacle predictions and guidance trajectories move on by one
+    sample (constant-velocity extrapolation at the end), the ego state is
+    `state_next`, and the planner bookkeeping comes from `carried`
+    (producers.Carried / the mpcg_advance outputs, host arrays)."""
+    obst = np.concatenate([sc.obst[:, :, 1:], 2 * sc.obst[:, :, -1:] - sc.obst[:, :, -2:-1]], 2)
+    obst[..., 2:5] = sc.obst[..., 2:5]
+    gd = np.concatenate([sc.guidance[:, :, 1:], sc.guidance[:, :, -1:]], 2)
+    gd[:, :, -1, 0:2] = sc.guidance[:, :, -1, 0:2] + layout.dt * sc.guidance[:, :, -1, 2:4]
+    return Scenes(stage_params=sc.stage_params.copy(), state=np.array(state_next, float), obst=obst,
+                  obst_meta=sc.obst_meta.copy(), guidance=gd, guided=sc.guided.copy(),
+                  prev_traj=np.array(carried.prev_traj, float), prev_elapsed=np.array(carried.prev_elapsed, float),
+                  consistency_on=np.array(carried.consistency_on, bool),
+                  previously_selected=np.array(carried.previously_selected, bool),
+                  main_warm=np.array(carried.main_warm, float))
