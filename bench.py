@@ -161,18 +161,25 @@ def main():
 
     bps = algorithmic_bytes_per_solve(lay)
     achieved = bps * B / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, f64 = None, None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("config") == args.config and tj.get("batch") == B:
                 traffic = tj.get("hbm_bytes_per_launch")
+                f64 = tj.get("fp64_issued_flop_per_launch")
         except Exception:
-            traffic = None
+            traffic, f64 = None, None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "sqp_kernel", "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps}
 
+    if f64:
+        # the path is fp64-VALU / latency bound: issued fp64 FLOP/s of the
+        # solve kernel (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, profiles/) against the vector peak
+        roofline["fp64_valu"] = {"achieved_tflops": round(f64 / (kern_ms * 1e-3) / 1e12, 3),
+                                 "peak_tflops": FP64_VALU_PEAK_TFLOPS,
+                                 "frac": f64 / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS}
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -16,4 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $o/prof_${tag}_wr
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
   -d $o/prof_${tag}_sq -o run --output-format csv \
   -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $o/prof_${tag}_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES \
+  -d $o/prof_${tag}_f64 -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $o/prof_${tag}_f64.log 2>&1
 echo profile-done

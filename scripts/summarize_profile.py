@@ -27,7 +27,7 @@ def counters(path):
     meta = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        key = "sqp_kernel" if "sqp_kernel" in name else ("select_best_kernel" if "select_best" in name else None)
+        key = next((k for k in ("sqp_kernel", "select_best_kernel", "prepare_kernel") if k in name), None)
         if key is None:
             continue
         agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--scenes", type=int, default=1024)
     ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--npar", type=int, default=138)
     args = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out")
     out = os.path.join(ROOT, "profiles")
@@ -50,7 +51,7 @@ def main():
     shutil.copy(os.path.join(src, f"prof_{tag}_trace", "run_kernel_stats.csv"),
                 os.path.join(out, f"{tag}_kernel_stats.csv"))
     pmc, meta = {}, {}
-    for p in ("fetch", "write", "sq"):
+    for p in ("fetch", "write", "sq", "f64"):
         f = os.path.join(src, f"prof_{tag}_{p}", "run_counter_collection.csv")
         if os.path.exists(f):
             c, m = counters(f)
@@ -70,21 +71,35 @@ def main():
                                                                  "SQ_ACTIVE_INST_LDS", "SQ_WAIT_ANY",
                                                                  "SQ_WAIT_INST_ANY") if c in d}
             e["cycles_per_wave"] = 4 * wc / d.get("SQ_WAVES", 1)
+        if "SQ_INSTS_VALU_FMA_F64" in d:
+            # wave-level instruction counts x 64 lanes (issued lanes, masked lanes included)
+            fl = 64 * (d.get("SQ_INSTS_VALU_ADD_F64", 0) + d.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                       2 * d["SQ_INSTS_VALU_FMA_F64"] + d.get("SQ_INSTS_VALU_TRANS_F64", 0))
+            e["fp64_issued_flop_per_launch"] = fl
         res["kernels"][k] = e
+    pk = res["kernels"].get("prepare_kernel")
+    if pk and "hbm_write_bytes" in pk:
+        # prepare_kernel streams params [B][N][npar], warm [B][N+1][7], xinit [B][5] (doubles),
+        # prev_interp [S][N][2] and the consistency flags [B] out exactly once
+        algo_w = 8 * args.batch * (args.N * args.npar + (args.N + 1) * 7 + 5) + 8 * args.scenes * args.N * 2 + args.batch
+        res["calibration_write"] = {"kernel": "prepare_kernel", "algorithmic_write_bytes": algo_w,
+                                    "write_size_bytes": pk["hbm_write_bytes"], "ratio": pk["hbm_write_bytes"] / algo_w}
     sb = res["kernels"].get("select_best_kernel")
     if sb and "hbm_read_bytes" in sb:
         # select_best reads xtraj (B*(N+1)*5 doubles; x, y of stages 1..N-2 touch every line), pobj (B doubles),
-        # exit (B int32), the consistency flags (B bytes) and prev_traj (S*N*2 doubles)
+        # exit (B int32), the consistency flags (B bytes) and prev_traj (S*N*2 doubles).  In the bench
+        # pipeline these were written by the two kernels before it and are largely L2-resident, so the
+        # ratio is a lower bound of the FETCH_SIZE correction, not a calibration of it.
         algo = 8 * (args.batch * (args.N + 1) * 5 + args.batch) + 4 * args.batch + args.batch + 8 * args.scenes * args.N * 2
-        res["calibration"] = {"kernel": "select_best_kernel", "algorithmic_read_bytes": algo,
-                              "corrected_fetch_bytes": sb["hbm_read_bytes"],
-                              "ratio": sb["hbm_read_bytes"] / algo}
+        res["select_best_reads"] = {"algorithmic_read_bytes": algo, "corrected_fetch_bytes": sb["hbm_read_bytes"],
+                                    "ratio": sb["hbm_read_bytes"] / algo}
     json.dump(res, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
     sq = res["kernels"].get("sqp_kernel", {})
     if "hbm_bytes_per_launch" in sq:
         json.dump({"tag": tag, "config": args.config, "batch": args.batch,
                    "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
-                   "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"]},
+                   "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"],
+                   "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch")},
                   open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
