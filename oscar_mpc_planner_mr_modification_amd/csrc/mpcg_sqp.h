@@ -5,11 +5,13 @@
 // `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:86-119).
 //
 // Lane layout (PARTS lanes per shooting stage, lane = k * PARTS + part):
-//   part 0 of stage k  cost / ERK4 / MIRROR / stage algebra of stage k and the
-//                      14 box-bound rows (input + state bounds); with PARTS == 2
-//                      also the first h rows
-//   parts >= 1         the nonlinear-constraint (h) rows of stage k, one shared
-//                      code path with a per-lane row offset
+//   part 0 of stage k  cost / ERK4 / MIRROR / stage algebra of stage k
+//   every part p       the inequality rows of stage k it owns: both bound rows
+//                      of the variables p, p + PARTS, ... and the h rows
+//                      p, p + PARTS, ...  All parts run the same code on
+//                      runtime row indices, so a row loop costs
+//                      ceil(7 / PARTS) * 2 + ceil(nh / PARTS) iterations
+//                      (12 for C2) whatever the part.
 // Every inequality row keeps its interior-point state (slack t, multiplier l,
 // 1/t, residual, predictor product) in REGISTERS of its owner lane for the
 // whole QP; LDS holds only the stage blocks (~37 KB per solve for N=20 ->
@@ -43,16 +45,12 @@ struct Cfg {
     static constexpr int NH = NL + NE;
     static constexpr int PARTS = (64 / (N + 1)) >= 3 ? 3 : 2;
     static_assert((N + 1) * PARTS <= 64, "horizon too long for one wavefront");
-    // h rows handled by part 0 (PARTS == 2 only, to balance the two lanes)
-    static constexpr int H0 = PARTS == 2 ? imax(0, (NH - NBOX) / 2) : 0;
-    // h rows per lane of class 1 (parts >= 1)
-    static constexpr int HC1 = PARTS == 2 ? NH - H0 : (NH + 1) / 2;
-    static constexpr int SLOTS0 = NBOX + H0;
-    static constexpr int SLOTS = imax(SLOTS0, HC1);
-    static constexpr int HSLOTS = imax(H0, HC1);
+    // rows of a lane: box slots j (variable part + PARTS j, lower and upper
+    // side: slots 2j, 2j + 1), then h slots r (h row part + PARTS r)
+    static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
+    static constexpr int HS = (NH + PARTS - 1) / PARTS;
+    static constexpr int SLOTS = 2 * BVS + HS;
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
-    // first h row of a class-1 lane
-    __host__ __device__ static constexpr int hoff(int part) { return PARTS == 2 ? H0 : (part - 1) * HC1; }
 };
 
 template <class C>
@@ -74,6 +72,7 @@ struct Lds {
     double P[N + 1][15];      // Riccati cost-to-go, packed
     double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
     double Y[N][NU][NX];      // L^-1 Mux
+    double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
     double Dg[N][C::NH][3];   // signed h-row gradients on (x, y, psi)
     double hd[N][C::NH];      // h-row bound gaps (uh - h or h - lh)
     double Msc[28];           // factorisation scratch
@@ -116,9 +115,6 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// box row s (0..13): variable and sign (lower bounds -1, upper +1)
-__host__ __device__ constexpr int box_var(int s) { return s < 2 * NU ? (s >> 1) : NU + ((s - 2 * NU) >> 1); }
-__host__ __device__ constexpr double box_sign(int s) { return (s & 1) ? 1.0 : -1.0; }
 
 // barrier contribution at (i, j), i >= j: diagonal part dh[0..6] plus the
 // (x, y, psi) block dh[7..12]
@@ -135,54 +131,40 @@ __device__ __forceinline__ double dh_at(const double* dh, int i, int j) {
 template <class C>
 struct Rows {
     double t[C::SLOTS], l[C::SLOTS], it[C::SLOTS], rin[C::SLOTS], pr[C::SLOTS];
-    double nlam[C::HSLOTS];  // NLP multiplier of the h row (Hessian weight of the next linearisation)
+    double nlam[C::HS];  // NLP multiplier of the h row (Hessian weight of the next linearisation)
 };
 
-// Row-class descriptors: class 0 = part 0 (box rows, then h rows [0, H0));
-// class 1 = parts >= 1 (h rows [hoff, hoff + HC1)).
-template <class C, int CL>
-struct RowClass {
-    static constexpr int NB = CL == 0 ? NBOX : 0;
-    static constexpr int NHR = CL == 0 ? C::H0 : C::HC1;
-    static constexpr int NS = NB + NHR;
+// The rows of the lane (stage k, part p): box slot j <-> variable v(j) = p + PARTS j,
+// h slot r <-> h row hh(r) = p + PARTS r.
+template <class C>
+struct LaneRows {
+    int k, part;
+    double lo[C::BVS], hi[C::BVS];
+    __device__ __forceinline__ int var(int j) const { return part + C::PARTS * j; }
+    __device__ __forceinline__ int hrow(int r) const { return part + C::PARTS * r; }
+    // input bounds on every stage < N, state bounds on 1..N-1
+    __device__ __forceinline__ bool box_on(int j) const {
+        const int v = var(j);
+        return v < NZ && (k == 0 ? v < NU : k < C::N);
+    }
+    __device__ __forceinline__ bool h_on(int r) const { return k >= 1 && k < C::N && hrow(r) < C::NH; }
 };
-
-// dispatch a generic lambda on the lane's row class (compile-time) + h offset
-template <class C, class Fn>
-__device__ __forceinline__ void on_class(int part, Fn&& fn) {
-    if (part == 0) fn(std::integral_constant<int, 0>{}, 0);
-    else fn(std::integral_constant<int, 1>{}, C::hoff(part));
-}
-
-// row s of class CL is active at stage k (h rows beyond NH are padding)
-template <class C, int CL>
-__device__ __forceinline__ bool row_active(int s, int k, int hoff) {
-    if (s < RowClass<C, CL>::NB) return (k == 0) ? (s < 2 * NU) : (k < C::N);
-    return k >= 1 && k < C::N && (hoff + s - RowClass<C, CL>::NB) < C::NH;
-}
-
-// D_row . v for row s (v in z-order)
-template <class C, int CL>
-__device__ __forceinline__ double row_dot(const double (*Dg)[3], int s, int hoff, const double v[NZ]) {
-    if (s < RowClass<C, CL>::NB) return box_sign(s) * v[box_var(s)];
-    const int hh = hoff + s - RowClass<C, CL>::NB;
-    return Dg[hh][0] * v[2] + Dg[hh][1] * v[3] + Dg[hh][2] * v[4];
-}
 
 // h values, signed gradients, bound gaps and the multiplier-weighted Hessian
 // (xx xy xp yy yp pp on x, y, psi) of the h rows of a lane at stage k.
-template <class C, int CL>
+template <class C>
 __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[NZ],
-                                       int hoff, const double* nlam, double hb6[6], double (*Dg)[3], double* hd) {
+                                       const LaneRows<C>& LR, const double* nlam, double hb6[6], double (*Dg)[3],
+                                       double* hd) {
     const double x = z[2], y = z[3], psi = z[4];
     const double rdisc = pk[pr.i_disc_r], off = pk[pr.i_disc_off];
     double sp, cp;
     sincos(psi, &sp, &cp);
     const double dxp = -off * sp, dyp = off * cp, dxpp = -off * cp, dypp = -off * sp;
 #pragma unroll
-    for (int r = 0; r < RowClass<C, CL>::NHR; ++r) {
-        const int hh = hoff + r;
-        if (hh >= C::NH) continue;
+    for (int r = 0; r < C::HS; ++r) {
+        if (!LR.h_on(r)) continue;
+        const int hh = LR.hrow(r);
         if (hh < C::NL) {
             // topology halfspace a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370)
             const double* c = pk + pr.i_lin0 + 3 * hh;
@@ -221,18 +203,6 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
     }
 }
 
-// bound gap of row s at stage k (box rows from the iterate, h rows from LDS)
-template <class C, int CL>
-__device__ __forceinline__ double row_gap(const mpcg_problem& pr, const double* zk, const double* hd, int s, int hoff) {
-    if (s < RowClass<C, CL>::NB) {
-        const int v = box_var(s);
-        const double lo = v < NU ? pr.lbu[v] : pr.lbx[v - NU];
-        const double hi = v < NU ? pr.ubu[v] : pr.ubx[v - NU];
-        return (s & 1) ? hi - zk[v] : zk[v] - lo;
-    }
-    return hd[hoff + s - RowClass<C, CL>::NB];
-}
-
 template <class C>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps) {
@@ -256,17 +226,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // NLP multipliers carried over from the previous solve of this planner
     // (zero for a fresh or reset acados capsule)
     const double* lam_in = io.lam_in ? io.lam_in + (size_t)sol * N * LAMS : nullptr;
+    constexpr int BVS = C::BVS, HS = C::HS, HB = 2 * C::BVS;  // HB: first h slot
+    LaneRows<C> LR;
+    LR.k = k;
+    LR.part = part;
+#pragma unroll
+    for (int j = 0; j < BVS; ++j) {
+        const int v = LR.var(j);
+        double lo = 0.0, hi = 0.0;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i)
+            if (v == i) { lo = i < NU ? pr.lbu[i] : pr.lbx[i - NU]; hi = i < NU ? pr.ubu[i] : pr.ubx[i - NU]; }
+        LR.lo[j] = lo;
+        LR.hi[j] = hi;
+    }
     Rows<C> R;
 #pragma unroll
-    for (int s = 0; s < C::HSLOTS; ++s) R.nlam[s] = 0.0;
-    if (lam_in && k >= 1 && k < N) {
-        on_class<C>(part, [&](auto Cc, int hoff) {
-            constexpr int CL = decltype(Cc)::value;
-#pragma unroll
-            for (int r = 0; r < RowClass<C, CL>::NHR; ++r)
-                if (hoff + r < C::NH) R.nlam[r] = lam_in[(size_t)k * LAMS + NX + hoff + r];
-        });
-    }
+    for (int r = 0; r < HS; ++r) R.nlam[r] = (lam_in && LR.h_on(r)) ? lam_in[(size_t)k * LAMS + NX + LR.hrow(r)] : 0.0;
 
     // ---- load warm start (loadWarmstart, acados_solver_interface.cpp:274-284)
     const double* w = io.warm + (size_t)sol * (N + 1) * NZ;
@@ -289,13 +265,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
             double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) {
-                on_class<C>(part, [&](auto Cc, int hoff) {
-                    constexpr int CL = decltype(Cc)::value;
-                    if constexpr (RowClass<C, CL>::NHR > 0)
-                        h_rows<C, CL>(pr, pk, zk, hoff, R.nlam, hb6, S.Dg[k], S.hd[k]);
-                });
-            }
+            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k]);
             STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {
@@ -357,21 +327,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         STAMP_BEGIN();
         // cold start: t = max(gap, thr0), l = mu0 / t
         {
-            double zk[NZ];
+            auto cold = [&](int s, double gap) {
+                const double t0 = gap > pr.qp_thr0 ? gap : pr.qp_thr0;
+                R.t[s] = t0;
+                R.l[s] = pr.qp_mu0 / t0;
+                R.pr[s] = 0.0;
+            };
 #pragma unroll
-            for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
-            on_class<C>(part, [&](auto Cc, int hoff) {
-                constexpr int CL = decltype(Cc)::value;
+            for (int j = 0; j < BVS; ++j) {
+                if (!LR.box_on(j)) continue;
+                const double zv = S.z[k][LR.var(j)];
+                cold(2 * j, zv - LR.lo[j]);
+                cold(2 * j + 1, LR.hi[j] - zv);
+            }
 #pragma unroll
-                for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                    if (!row_active<C, CL>(s, k, hoff)) continue;
-                    const double gap = row_gap<C, CL>(pr, zk, S.hd[kc], s, hoff);
-                    const double t0 = gap > pr.qp_thr0 ? gap : pr.qp_thr0;
-                    R.t[s] = t0;
-                    R.l[s] = pr.qp_mu0 / t0;
-                    R.pr[s] = 0.0;
-                }
-            });
+            for (int r = 0; r < HS; ++r)
+                if (LR.h_on(r)) cold(HB + r, S.hd[k][LR.hrow(r)]);
         }
         if (stage_lane) {
 #pragma unroll
@@ -394,34 +365,46 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 double zk[NZ], dzk[NZ];
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) { dzk[i] = S.dz[ks][i]; zk[i] = S.z[ks][i]; }
-                double rbox[NZ] = {0, 0, 0, 0, 0, 0, 0}, rh[3] = {0, 0, 0};
-                on_class<C>(part, [&](auto Cc, int hoff) {
-                    constexpr int CL = decltype(Cc)::value;
+                double rh[3] = {0, 0, 0};
+                auto row_res = [&](int s, double ddot, double gap) {
+                    const double l = R.l[s], t = R.t[s];
+                    const double rin = ddot + t - gap;
+                    R.rin[s] = rin;
+                    R.it[s] = frcp(t);
+                    ri = fmax(ri, fabs(rin));
+                    comp += l * t;
+                };
 #pragma unroll
-                    for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                        if (!row_active<C, CL>(s, k, hoff)) continue;
-                        const double l = R.l[s], t = R.t[s];
-                        if (s < RowClass<C, CL>::NB) {
-                            rbox[box_var(s)] += box_sign(s) * l;
-                        } else {
-                            const int hh = hoff + s - RowClass<C, CL>::NB;
-                            rh[0] += S.Dg[k][hh][0] * l; rh[1] += S.Dg[k][hh][1] * l; rh[2] += S.Dg[k][hh][2] * l;
-                        }
-                        const double rin = row_dot<C, CL>(S.Dg[kc], s, hoff, dzk) + t -
-                                           row_gap<C, CL>(pr, zk, S.hd[kc], s, hoff);
-                        R.rin[s] = rin;
-                        R.it[s] = frcp(t);
-                        ri = fmax(ri, fabs(rin));
-                        comp += l * t;
+                for (int j = 0; j < BVS; ++j) {
+                    double rb = 0.0;
+                    if (LR.box_on(j)) {
+                        const int v = LR.var(j);
+                        const double zv = S.z[k][v], dzv = S.dz[k][v];
+                        rb = R.l[2 * j + 1] - R.l[2 * j];
+                        row_res(2 * j, -dzv, zv - LR.lo[j]);
+                        row_res(2 * j + 1, dzv, LR.hi[j] - zv);
                     }
-                });
+                    if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = rb;
+                }
+#pragma unroll
+                for (int r = 0; r < HS; ++r) {
+                    if (!LR.h_on(r)) continue;
+                    const int hh = LR.hrow(r);
+                    const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2], l = R.l[HB + r];
+                    rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;
+                    row_res(HB + r, a * dzk[2] + bq * dzk[3] + c * dzk[4], S.hd[k][hh]);
+                }
                 double acc[3] = {rh[0], rh[1], rh[2]};
 #pragma unroll
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
                     for (int i = 0; i < 3; ++i) acc[i] += __shfl_down(rh[i], p);
-                rbox[2] += acc[0]; rbox[3] += acc[1]; rbox[4] += acc[2];
+                __syncthreads();  // the owner lanes' box sums S.bx
                 if (stage_lane) {
+                    double rbox[NZ];
+#pragma unroll
+                    for (int i = 0; i < NZ; ++i) rbox[i] = S.bx[k][i];
+                    rbox[2] += acc[0]; rbox[3] += acc[1]; rbox[4] += acc[2];
                     double r[NZ];
 #pragma unroll
                     for (int i = 0; i < NZ; ++i) {
@@ -474,31 +457,42 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 // ---- barrier terms + Newton gradient
                 STAMP_BEGIN();
                 {
-                    double qb[NZ] = {0, 0, 0, 0, 0, 0, 0}, dd[NZ] = {0, 0, 0, 0, 0, 0, 0};
                     double qh[3] = {0, 0, 0}, dbh[6] = {0, 0, 0, 0, 0, 0};
-                    on_class<C>(part, [&](auto Cc, int hoff) {
-                        constexpr int CL = decltype(Cc)::value;
+                    // coef = l + (l rin - rc) / t, wgt = l / t of slot s
+                    auto bar = [&](int s, double& coef, double& wgt) {
+                        const double l = R.l[s], t = R.t[s], itt = R.it[s];
+                        const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
+                        coef = l + (l * R.rin[s] - rc) * itt;
+                        wgt = l * itt;
+                    };
 #pragma unroll
-                        for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                            if (!row_active<C, CL>(s, k, hoff)) continue;
-                            const double l = R.l[s], t = R.t[s], itt = R.it[s];
-                            const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
-                            const double coef = l + (l * R.rin[s] - rc) * itt;
-                            const double wgt = l * itt;
-                            if (s < RowClass<C, CL>::NB) {
-                                qb[box_var(s)] += box_sign(s) * coef;
-                                dd[box_var(s)] += wgt;
-                            } else {
-                                const int hh = hoff + s - RowClass<C, CL>::NB;
-                                const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
-                                qh[0] += a * coef; qh[1] += bq * coef; qh[2] += c * coef;
-                                if (phase == 0) {
-                                    dbh[0] += a * wgt * a; dbh[1] += a * wgt * bq; dbh[2] += a * wgt * c;
-                                    dbh[3] += bq * wgt * bq; dbh[4] += bq * wgt * c; dbh[5] += c * wgt * c;
-                                }
-                            }
+                    for (int j = 0; j < BVS; ++j) {
+                        double qb = 0.0, dd = 0.0;
+                        if (LR.box_on(j)) {
+                            double c0, w0, c1, w1;
+                            bar(2 * j, c0, w0);
+                            bar(2 * j + 1, c1, w1);
+                            qb = c1 - c0;
+                            dd = w0 + w1;
                         }
-                    });
+                        if (k <= N && LR.var(j) < NZ) {
+                            S.bx[k][LR.var(j)] = qb;
+                            if (phase == 0) S.dH[k][LR.var(j)] = dd;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < HS; ++r) {
+                        if (!LR.h_on(r)) continue;
+                        const int hh = LR.hrow(r);
+                        double coef, wgt;
+                        bar(HB + r, coef, wgt);
+                        const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
+                        qh[0] += a * coef; qh[1] += bq * coef; qh[2] += c * coef;
+                        if (phase == 0) {
+                            dbh[0] += a * wgt * a; dbh[1] += a * wgt * bq; dbh[2] += a * wgt * c;
+                            dbh[3] += bq * wgt * bq; dbh[4] += bq * wgt * c; dbh[5] += c * wgt * c;
+                        }
+                    }
                     double aq[3] = {qh[0], qh[1], qh[2]}, ab[6];
 #pragma unroll
                     for (int i = 0; i < 6; ++i) ab[i] = dbh[i];
@@ -511,13 +505,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int i = 0; i < 6; ++i) ab[i] += __shfl_down(dbh[i], p);
                         }
                     }
+                    __syncthreads();  // the owner lanes' box sums S.bx
                     if (stage_lane) {
 #pragma unroll
-                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[i] + S.g[k][i] + qb[i];
+                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[i] + S.g[k][i] + S.bx[k][i];
                         S.q[k][2] += aq[0]; S.q[k][3] += aq[1]; S.q[k][4] += aq[2];
                         if (phase == 0) {
-#pragma unroll
-                            for (int i = 0; i < NZ; ++i) S.dH[k][i] = dd[i];
 #pragma unroll
                             for (int i = 0; i < 6; ++i) S.dH[k][NZ + i] = ab[i];
                         }
@@ -727,43 +720,46 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     for (int i = 0; i < NZ; ++i) ddk[i] = S.ddz[ks][i];
                     const double smu = sigma_mu;
                     const int ph = phase;
+                    // per-row D . ddz of the lane's rows
+                    double ddb[BVS];
+#pragma unroll
+                    for (int j = 0; j < BVS; ++j) ddb[j] = LR.box_on(j) ? S.ddz[k][LR.var(j)] : 0.0;
+                    auto ddot = [&](int s) {
+                        if (s < HB) return (s & 1) ? ddb[s >> 1] : -ddb[s >> 1];
+                        const int hh = LR.hrow(s - HB);
+                        return S.Dg[k][hh][0] * ddk[2] + S.Dg[k][hh][1] * ddk[3] + S.Dg[k][hh][2] * ddk[4];
+                    };
+                    auto active = [&](int s) { return s < HB ? LR.box_on(s >> 1) : LR.h_on(s - HB); };
                     // dt = -rin - D ddz; dl = -(rc + l dt) / t
-                    auto row_step = [&](auto Cc, int hoff, int s, double& dt, double& dl) {
-                        constexpr int CL = decltype(Cc)::value;
+                    auto row_step = [&](int s, double& dt, double& dl) {
                         const double l = R.l[s], t = R.t[s];
                         const double rc = (ph == 0) ? l * t : l * t + R.pr[s] - smu;
-                        dt = -R.rin[s] - row_dot<C, CL>(S.Dg[kc], s, hoff, ddk);
+                        dt = -R.rin[s] - ddot(s);
                         dl = -(rc + l * dt) * R.it[s];
                     };
                     // step to the boundary: min over rows of -t/dt and -l/dl = 1 / max(-dt/t, -dl/l)
                     double rmax = 0.0;
-                    on_class<C>(part, [&](auto Cc, int hoff) {
-                        constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                        for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                            if (!row_active<C, CL>(s, k, hoff)) continue;
-                            double dt, dl;
-                            row_step(Cc, hoff, s, dt, dl);
-                            rmax = fmax(rmax, -dt * R.it[s]);
-                            if (dl < 0.0) rmax = fmax(rmax, -dl * frcp(R.l[s]));
-                        }
-                    });
+                    for (int s = 0; s < C::SLOTS; ++s) {
+                        if (!active(s)) continue;
+                        double dt, dl;
+                        row_step(s, dt, dl);
+                        rmax = fmax(rmax, -dt * R.it[s]);
+                        if (dl < 0.0) rmax = fmax(rmax, -dl * frcp(R.l[s]));
+                    }
                     rmax = wave_max(rmax);
                     const double amax = rmax > 0.0 ? frcp(rmax) : 1e300;
                     if (phase == 0) {
                         const double aa = fmin(amax, 1.0);
                         double ca = 0.0;
-                        on_class<C>(part, [&](auto Cc, int hoff) {
-                            constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                            for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                                if (!row_active<C, CL>(s, k, hoff)) continue;
-                                double dt, dl;
-                                row_step(Cc, hoff, s, dt, dl);
-                                ca += (R.l[s] + aa * dl) * (R.t[s] + aa * dt);
-                                R.pr[s] = dt * dl;
-                            }
-                        });
+                        for (int s = 0; s < C::SLOTS; ++s) {
+                            if (!active(s)) continue;
+                            double dt, dl;
+                            row_step(s, dt, dl);
+                            ca += (R.l[s] + aa * dl) * (R.t[s] + aa * dt);
+                            R.pr[s] = dt * dl;
+                        }
                         ca = wave_sum(ca);
                         const double mu_aff = ca / C::M_TOTAL;
                         double sig = mu_aff / mu;
@@ -775,17 +771,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         if (alpha > 1.0) alpha = 1.0;
                         if (alpha >= 1e-12) {
                             // rows move with the corrector step (rin, ddz of the current iterate)
-                            on_class<C>(part, [&](auto Cc, int hoff) {
-                                constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                                for (int s = 0; s < RowClass<C, CL>::NS; ++s) {
-                                    if (!row_active<C, CL>(s, k, hoff)) continue;
-                                    double dt, dl;
-                                    row_step(Cc, hoff, s, dt, dl);
-                                    R.t[s] += alpha * dt;
-                                    R.l[s] += alpha * dl;
-                                }
-                            });
+                            for (int s = 0; s < C::SLOTS; ++s) {
+                                if (!active(s)) continue;
+                                double dt, dl;
+                                row_step(s, dt, dl);
+                                R.t[s] += alpha * dt;
+                                R.l[s] += alpha * dl;
+                            }
                         }
                     }
                 }
@@ -825,14 +818,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < NX; ++i) S.pi_nlp[k][i] = S.piq[k][i];
             }
         }
-        if (k >= 1 && k < N) {
-            on_class<C>(part, [&](auto Cc, int hoff) {
-                constexpr int CL = decltype(Cc)::value;
-                constexpr int NB = RowClass<C, CL>::NB;
 #pragma unroll
-                for (int s = NB; s < RowClass<C, CL>::NS; ++s) R.nlam[s - NB] = R.l[s];
-            });
-        }
+        for (int r = 0; r < HS; ++r)
+            if (LR.h_on(r)) R.nlam[r] = R.l[HB + r];
         __syncthreads();
         acados_status = AC_SUCCESS;
         if (qstat != AC_SUCCESS) break;
@@ -857,12 +845,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         if (k == 0) {
             for (int r = part; r < C::NH; r += PARTS) lo[NX + r] = 0.0;
         } else if (k < N) {
-            on_class<C>(part, [&](auto Cc, int hoff) {
-                constexpr int CL = decltype(Cc)::value;
 #pragma unroll
-                for (int r = 0; r < RowClass<C, CL>::NHR; ++r)
-                    if (hoff + r < C::NH) lo[(size_t)k * LAMS + NX + hoff + r] = R.nlam[r];
-            });
+            for (int r = 0; r < HS; ++r)
+                if (LR.h_on(r)) lo[(size_t)k * LAMS + NX + LR.hrow(r)] = R.nlam[r];
         }
     }
     if (lane == 0) {
