@@ -124,7 +124,7 @@ extern "C" {
 
 int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
 
-/* diagnostic builds only: device buffer of batch x 16 u64 phase-cycle sums */
+/* diagnostic builds only: device buffer of batch x 20 u64 phase-cycle sums */
 void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps = dev_ptr; }
 
 const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }

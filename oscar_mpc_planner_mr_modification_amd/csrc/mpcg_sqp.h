@@ -61,7 +61,7 @@ struct Lds {
     double g[N + 1][NZ];
     double F[N][NX][NZ];      // [B A]
     double b[N][NX];          // shooting defects
-    double dH[N + 1][13];     // barrier terms: diag(7) + (x,y,psi) block packed xx xy xp yy yp pp
+    double dH[N + 1][14];     // barrier terms: diag(7) + (x,y,psi) block packed xx xy xp yy yp pp, [13] = 0
     double q[N + 1][NZ];      // Newton gradient
     double dz[N + 1][NZ];     // QP iterate
     double ddz[N + 1][NZ];    // QP step
@@ -83,7 +83,7 @@ struct Lds {
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
 // production build compiles them out).  Read shares, not absolute times.
 #ifdef MPCG_STAMPS
-#define MPCG_NSTAMP 16
+#define MPCG_NSTAMP 20
 #define STAMP_DECL unsigned long long st_acc_[MPCG_NSTAMP] = {}, st_t0_ = 0, st_l_ = 0;
 #define STAMP_BEGIN() do { __syncthreads(); st_t0_ = __builtin_amdgcn_s_memtime(); st_l_ = st_t0_; } while (0)
 #define STAMP_END(i) do { __syncthreads(); st_acc_[i] += __builtin_amdgcn_s_memtime() - st_t0_; } while (0)
@@ -250,6 +250,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     if (lane < NX) S.xinit[lane] = io.xinit[(size_t)sol * NX + lane];
     for (int e = lane; e < N * NX; e += 64)
         (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
+    for (int e = lane; e <= N; e += 64) S.dH[e][13] = 0.0;
     __syncthreads();
     if (lane < NU) S.z[N][lane] = 0.0;
     __syncthreads();
@@ -525,8 +526,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     int ei = 0;
                     while ((ei + 1) * (ei + 2) / 2 <= lane && ei < 6) ++ei;
                     const int ej = lane < 28 ? lane - ei * (ei + 1) / 2 : 0;
-                    const int dhd = (ei == ej) ? ei : -1;
-                    int dhb = -1;
+                    // barrier entries of (ei, ej); 13 is the always-zero slot
+                    const int dhd = (ei == ej) ? ei : 13;
+                    int dhb = 13;
                     if (ei >= 2 && ei <= 4 && ej >= 2 && ej <= 4) {
                         const int a = ei - 2, c = ej - 2;
                         dhb = NZ + ((c == 0) ? a : (c == 1 ? 2 + a : 5));
@@ -543,12 +545,18 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double fi[NX], fj[NX], hv;
 #pragma unroll
                     for (int m = 0; m < NX; ++m) { fi[m] = S.F[N - 1][m][ei]; fj[m] = S.F[N - 1][m][ej]; }
-                    hv = S.H[N - 1][le] + (dhd >= 0 ? S.dH[N - 1][dhd] : 0.0) + (dhb >= 0 ? S.dH[N - 1][dhb] : 0.0);
+                    hv = S.H[N - 1][le] + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
 #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
                         double Pm[15];
 #pragma unroll
                         for (int e = 0; e < 15; ++e) Pm[e] = S.P[kk + 1][e];
+                        // prefetch the next (lower) stage's block; it lands while this one is reduced
+                        const int kn = kk > 0 ? kk - 1 : 0;
+                        double fi2[NX], fj2[NX];
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) { fi2[m] = S.F[kn][m][ei]; fj2[m] = S.F[kn][m][ej]; }
+                        const double hv2 = S.H[kn][le] + S.dH[kn][dhd] + S.dH[kn][dhb];
                         double v = hv;
 #pragma unroll
                         for (int m = 0; m < NX; ++m) {
@@ -558,12 +566,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             v += fi[m] * tm;
                         }
                         if (lane < 28) S.Msc[lane] = v;
-                        // prefetch the next (lower) stage while this one is reduced
-                        const int kn = kk > 0 ? kk - 1 : 0;
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) { fi[m] = S.F[kn][m][ei]; fj[m] = S.F[kn][m][ej]; }
-                        hv = S.H[kn][le] + (dhd >= 0 ? S.dH[kn][dhd] : 0.0) + (dhb >= 0 ? S.dH[kn][dhb] : 0.0);
+                        for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
+                        hv = hv2;
+                        STAMP_LAP(16);
                         __syncthreads();
+                        STAMP_LAP(17);
                         if (lane < 15) {
                             const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
                             // 2x2 Cholesky through reciprocal square roots
@@ -581,7 +589,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             if (pj_ == 0) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
                             if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
                         }
+                        STAMP_LAP(18);
                         __syncthreads();
+                        STAMP_LAP(19);
                     }
                     if (S.flag) { qstat = AC_NAN; break; }
                 }
