@@ -93,6 +93,14 @@ void orc_stage_cost(const orc_problem *pr, const double *z, const double *p,
     g[1] += 2.0 * ww * w; H[1][1] += 2.0 * ww;
     L += wv * (v - vref) * (v - vref);
     g[5] += 2.0 * wv * (v - vref); H[5][5] += 2.0 * wv;
+#if ORC_NX > 5
+    /* slack weight (generate_jackalsimulator_solver.py:78) */
+    if (pr->i_w_slack >= 0) {
+        double ws = p[pr->i_w_slack], sl = z[NU + 5];
+        L += ws * sl * sl;
+        g[NU + 5] += 2.0 * ws * sl; H[NU + 5][NU + 5] += 2.0 * ws;
+    }
+#endif
 
     /* Contouring (contouring.py:140-174), stage_idx=1 => no terminal terms */
     double lam[ORC_MAX_SEG][3];
@@ -149,12 +157,16 @@ void orc_stage_cost(const orc_problem *pr, const double *z, const double *p,
 /* ------------------------------------------------------------------ */
 /* Constraints h(z) (solver_definition.py:37-49)                      */
 /* ------------------------------------------------------------------ */
-int orc_num_h(const orc_problem *pr) { return pr->n_lin + pr->n_ell; }
+int orc_nx(void) { return ORC_NX; }
+
+int orc_num_h(const orc_problem *pr) { return pr->n_lin + pr->n_ell + pr->n_scen; }
 
 void orc_h_bounds(const orc_problem *pr, double *lh, double *uh) {
     /* guidance_constraints.py:343-353: (-inf, 0]; ellipsoid_constraints.py:421-433: [1, inf) */
     for (int i = 0; i < pr->n_lin; i++) { lh[i] = -BIGBOUND; uh[i] = 0.0; }
     for (int j = 0; j < pr->n_ell; j++) { lh[pr->n_lin + j] = 1.0; uh[pr->n_lin + j] = BIGBOUND; }
+    /* scenario_constraints.py:55-65: (-inf, 0] */
+    for (int i = 0; i < pr->n_scen; i++) { lh[pr->n_lin + pr->n_ell + i] = -BIGBOUND; uh[pr->n_lin + pr->n_ell + i] = 0.0; }
 }
 
 void orc_stage_constraints(const orc_problem *pr, const double *z, const double *p,
@@ -171,7 +183,7 @@ void orc_stage_constraints(const orc_problem *pr, const double *z, const double 
         jac[i * NZ + 3] = c[1];
     }
     /* obstacle ellipsoids d' R' D R d >= 1 (ellipsoid_constraints.py:435-489), one disc */
-    double rd = p[pr->i_disc_r], off = p[pr->i_disc_off];
+    double rd = pr->i_disc_r >= 0 ? p[pr->i_disc_r] : 0.0, off = pr->i_disc_off >= 0 ? p[pr->i_disc_off] : 0.0;
     double cp = cos(psi), sp = sin(psi);
     double dxp = -off * sp, dyp = off * cp;       /* d(disc)/dpsi */
     double dxpp = -off * cp, dypp = -off * sp;    /* d2(disc)/dpsi2 */
@@ -205,6 +217,19 @@ void orc_stage_constraints(const orc_problem *pr, const double *z, const double 
                              2.0 * (Mdx * dxpp + Mdy * dypp);
         }
     }
+    /* scenario halfspaces a1 xd + a2 yd - (b + slack) <= 0 at the disc position
+     * (x, y) + R(psi) (offset, 0) (scenario_constraints.py:64-94) */
+    for (int i = 0; i < pr->n_scen; i++) {
+        const double *c = p + pr->i_scen0 + 3 * i;
+        int r = pr->n_lin + pr->n_ell + i;
+        double sl = (NX > 5) ? z[NU + NX - 1] : 0.0;
+        h[r] = c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl);
+        jac[r * NZ + 2] = c[0];
+        jac[r * NZ + 3] = c[1];
+        jac[r * NZ + 4] = c[0] * dxp + c[1] * dyp;
+        if (NX > 5) jac[r * NZ + NU + NX - 1] = -1.0;
+        if (hess) hess[(size_t)r * NZ * NZ + 4 * NZ + 4] = c[0] * dxpp + c[1] * dypp;
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -214,6 +239,7 @@ void orc_dynamics(const double *z, double *f, double *jac, double *hess) {
     double a = z[0], w = z[1], psi = z[4], v = z[5];
     double c = cos(psi), s = sin(psi);
     f[0] = v * c; f[1] = v * s; f[2] = w; f[3] = a; f[4] = v;
+    for (int i = 5; i < NX; i++) f[i] = 0.0; /* slack: constant (solver_model.py:287-294) */
     if (jac) {
         memset(jac, 0, sizeof(double) * NX * NZ);
         jac[0 * NZ + 4] = -v * s; jac[0 * NZ + 5] = c;
@@ -726,7 +752,7 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
     int N = pr->N, npar = pr->npar;
     int nh = orc_num_h(pr);
     int maxi = 2 * NZ + 2 * nh;
-    double lh[ORC_MAX_LIN + ORC_MAX_ELL], uh[ORC_MAX_LIN + ORC_MAX_ELL];
+    double lh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], uh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN];
     orc_h_bounds(pr, lh, uh);
 
     qp_ws w;
@@ -764,7 +790,7 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
         }
     }
 
-    double h[ORC_MAX_LIN + ORC_MAX_ELL], jac[(ORC_MAX_LIN + ORC_MAX_ELL) * NZ];
+    double h[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], jac[(ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN) * NZ];
     double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0;
     double res_eq = 0.0;

@@ -22,6 +22,10 @@ UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -12.566370614359172, -0.01, -1.0)
 UNICYCLE_UB = (2.0, 0.8, 2000.0, 2000.0, 12.566370614359172, 3.0, 10000.0)
 UNICYCLE_STATES = ("x", "y", "psi", "v", "spline")
 UNICYCLE_INPUTS = ("a", "w")
+# ContouringSecondOrderUnicycleModelWithSlack (solver_model.py:274-285): + slack state in [0, 5000]
+SLACK_LB = UNICYCLE_LB + (0.0,)
+SLACK_UB = UNICYCLE_UB + (5000.0,)
+SLACK_STATES = UNICYCLE_STATES + ("slack",)
 
 
 class _Params:
@@ -77,6 +81,15 @@ def _guidance_linear(p: _Params, n: int):
         p.add(f"lin_constraint_{i}_b", "lin_constraint_b")
 
 
+def _scenario(p: _Params, n_discs: int, n_constraints: int):
+    # scenario_constraints.py:41-50
+    for d in range(n_discs):
+        p.add(f"ego_disc_{d}_offset", "ego_disc_offset")
+        for i in range(n_constraints * n_discs):
+            for c in ("a1", "a2", "b"):
+                p.add(f"disc_{d}_scenario_constraint_{i}_{c}")
+
+
 def _ellipsoid(p: _Params, n_discs: int, n_obs: int):
     # ellipsoid_constraints.py:406-419
     p.add("ego_disc_radius")
@@ -97,6 +110,8 @@ class Layout:
     n_ell: int
     n_seg: int = 5
     consistency: bool = True
+    model: str = "unicycle"      # or "unicycle_slack" (slack state last)
+    n_scen: int = 0
     dt: float = 0.2
     rk_steps: int = 3
     sqp_iters: int = 10
@@ -109,7 +124,7 @@ class Layout:
 
     @property
     def nx(self) -> int:
-        return 5
+        return 6 if self.model == "unicycle_slack" else 5
 
     @property
     def nu(self) -> int:
@@ -117,11 +132,23 @@ class Layout:
 
     @property
     def nvar(self) -> int:
-        return 7
+        return self.nx + self.nu
 
     @property
     def nh(self) -> int:
-        return self.n_lin + self.n_ell
+        return self.n_lin + self.n_ell + self.n_scen
+
+    @property
+    def states(self):
+        return SLACK_STATES if self.model == "unicycle_slack" else UNICYCLE_STATES
+
+    @property
+    def lb(self):
+        return SLACK_LB if self.model == "unicycle_slack" else UNICYCLE_LB
+
+    @property
+    def ub(self):
+        return SLACK_UB if self.model == "unicycle_slack" else UNICYCLE_UB
 
     def idx(self, name: str) -> int:
         return self.pmap.get(name, -1)
@@ -137,6 +164,8 @@ class Layout:
             i_lin0=g("lin_constraint_0_a1") if self.n_lin else -1,
             i_disc_r=g("ego_disc_radius"), i_disc_off=g("ego_disc_0_offset"),
             i_ell0=g("ellipsoid_obst_0_x") if self.n_ell else -1,
+            i_scen0=g("disc_0_scenario_constraint_0_a1") if self.n_scen else -1,
+            i_w_slack=g("slack"),
         )
 
 
@@ -165,6 +194,19 @@ def lmpcc_layout(N: int = 20, max_obstacles: int = 4, num_segments: int = 5) -> 
                   pmap=p.map, bundles=p.bundles)
 
 
+def safe_horizon_layout(N: int = 20, n_constraints: int = 24, num_segments: int = 5) -> Layout:
+    """configuration_safe_horizon (generate_jackalsimulator_solver.py:69-89): MPCBase(a, w, slack, v) +
+    Contouring + ScenarioConstraints on ContouringSecondOrderUnicycleModelWithSlack."""
+    p = _Params()
+    for n in ("acceleration", "angular_velocity", "slack", "velocity", "reference_velocity"):
+        p.add(n)
+    _contouring(p, num_segments)
+    _scenario(p, 1, n_constraints)
+    return Layout(name=f"shmpc_N{N}_scen{n_constraints}", N=N, max_obstacles=0, n_lin=0, n_ell=0,
+                  n_seg=num_segments, consistency=False, model="unicycle_slack", n_scen=n_constraints,
+                  pmap=p.map, bundles=p.bundles)
+
+
 # BASELINE.json configs on the unicycle T-MPC problem
 def config_layout(cfg: str) -> Layout:
     cfg = cfg.upper()
@@ -174,4 +216,8 @@ def config_layout(cfg: str) -> Layout:
         return tmpc_layout(N=20, max_obstacles=8, name="C2")
     if cfg == "C4":
         return tmpc_layout(N=30, max_obstacles=12, name="C4")
-    raise KeyError(f"config {cfg} has no unicycle layout (C3/C5 are later rows of SURVEY §8f)")
+    if cfg == "C5":
+        lay = safe_horizon_layout(N=20, n_constraints=24)
+        lay.name = "C5"
+        return lay
+    raise KeyError(f"config {cfg} has no layout (C3, the bicycle CA-MPC problem, is not built)")

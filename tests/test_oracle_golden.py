@@ -1,7 +1,7 @@
 """Pin the CPU oracle against the reference's own problem definition.
 
-Golden vectors: tests/golden/stage_{C1,C2}.npz, produced by
-tests/golden/gen_golden.py from the reference's Python modules
+Golden vectors: tests/golden/stage_{C1,C2,C5}.npz, produced by
+tests/golden/gen_golden.py (C5: gen_golden_c5.py) from the reference's Python modules
 (solver_generator/ + mpc_planner_modules/scripts/) through a sympy stand-in
 for casadi.  Parameter maps: tests/golden/parameter_maps.json from the
 reference's `define_parameters` (solver_definition.py:5-16).
@@ -30,6 +30,16 @@ def test_layout_matches_reference_parameter_map(maps, cfg):
     assert lay.npar == {"C1": 98, "C2": 138, "C4": 178}[cfg]   # SURVEY.md §8 dims
 
 
+def test_c5_layout_matches_reference_parameter_map():
+    """configuration_safe_horizon (generate_jackalsimulator_solver.py:69-89)"""
+    with open(os.path.join(GOLDEN, "parameter_maps_c5.json")) as fh:
+        m = json.load(fh)
+    lay = config_layout("C5")
+    assert lay.pmap == m["C5"]
+    assert lay.bundles == m["C5_bundles"]
+    assert (lay.npar, lay.nx, lay.nh) == (127, 6, 24)
+
+
 def test_layout_without_consistency(maps):
     lay = tmpc_layout(N=20, max_obstacles=4, consistency=False)
     assert lay.pmap == maps["C1_no_consistency"]
@@ -41,7 +51,7 @@ def test_reference_known_answer_counts(maps):
     assert len(maps["ellipsoid1"]) == 7 + 2
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C1"])
+@pytest.mark.parametrize("cfg", ["C2", "C1", "C5"])
 def test_stage_functions_match_golden(oracle_mod, cfg):
     lay = config_layout(cfg)
     o = oracle_mod.Oracle(lay)
@@ -70,6 +80,10 @@ def test_model_bounds_match_golden(oracle_mod):
     d = np.load(os.path.join(GOLDEN, "stage_C2.npz"))
     np.testing.assert_allclose(UNICYCLE_LB, d["model_lb"], rtol=0, atol=1e-15)
     np.testing.assert_allclose(UNICYCLE_UB, d["model_ub"], rtol=0, atol=1e-15)
+    d5 = np.load(os.path.join(GOLDEN, "stage_C5.npz"))
+    lay = config_layout("C5")
+    np.testing.assert_allclose(lay.lb, d5["model_lb"], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(lay.ub, d5["model_ub"], rtol=0, atol=1e-15)
 
 
 def test_ellipsoid_known_answer(oracle_mod):
