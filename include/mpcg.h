@@ -27,10 +27,14 @@
 extern "C" {
 #endif
 
+/* ContouringSecondOrderUnicycleModel (solver_model.py:185-214): nx 5.  The
+ * SH-MPC model ContouringSecondOrderUnicycleModelWithSlack (:274-298) adds the
+ * slack state last: nx 6.  Every buffer below is sized by mpcg_problem.nx. */
 #define MPCG_NX 5
+#define MPCG_MAX_NX 6
 #define MPCG_NU 2
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 2
+#define MPCG_ABI_VERSION 3
 
 /* Problem description: the generated solver's dimensions + the parameter
  * map (parameter_map.yaml written by solver_generator/generate_solver.py:34-46)
@@ -46,9 +50,13 @@ typedef struct mpcg_problem {
     int i_lin0;                    /* halfspace i at i_lin0 + 3 i: a1 a2 b */
     int i_disc_r, i_disc_off;
     int i_ell0;                    /* obstacle j at i_ell0 + 7 j: x y psi major minor chi r */
+    int n_scen, i_scen0;           /* scenario halfspace i at i_scen0 + 3 i: a1 a2 b
+                                      (a1 xd + a2 yd - (b + slack) <= 0, scenario_constraints.py:64-94) */
+    int i_w_slack;                 /* MPCBase weight of the slack state (nx 6) */
+    int nx;                        /* 5, or 6 with the slack state */
     double dt;                     /* integrator_step; ERK4 over dt with rk_steps steps */
     int rk_steps;
-    double lbu[MPCG_NU], ubu[MPCG_NU], lbx[MPCG_NX], ubx[MPCG_NX];
+    double lbu[MPCG_NU], ubu[MPCG_NU], lbx[MPCG_MAX_NX], ubx[MPCG_MAX_NX];
     int sqp_iters;                 /* solver_settings.acados.iterations (timeout disabled) */
     double qp_tol;                 /* 1e-5 */
     int qp_iter_max;               /* 50 */
@@ -64,7 +72,7 @@ typedef struct mpcg_problem {
 int mpcg_abi_version(void);
 const char *mpcg_last_error(void);
 
-/* Number of nonlinear-constraint rows per stage (n_lin + n_ell). */
+/* Number of nonlinear-constraint rows per stage (n_lin + n_ell + n_scen). */
 int mpcg_num_h(const mpcg_problem *pr);
 
 /* Size in doubles of one solve's multiplier block: N * (nx + nh). */
@@ -74,12 +82,14 @@ int mpcg_lam_size(const mpcg_problem *pr);
  * parameter_map.yaml) and the solver settings: the module bundles are found
  * by the names the reference's generator gives them (mpc_base.py, contouring.py,
  * consistency_module.py, guidance_constraints.py:333-338,
- * ellipsoid_constraints.py:406-419); n_lin / n_ell / n_seg are counted from
- * `lin_constraint_<i>_a1`, `ellipsoid_obst_<j>_x`, `spline<i>_start`.
- * lb/ub: nvar bounds in z order [u x] (model_map.yaml columns 3, 4).
+ * ellipsoid_constraints.py:406-419, scenario_constraints.py:41-50); n_lin /
+ * n_ell / n_scen / n_seg are counted from `lin_constraint_<i>_a1`,
+ * `ellipsoid_obst_<j>_x`, `disc_0_scenario_constraint_<i>_a1`, `spline<i>_start`.
+ * nx: 5, or 6 for the model with the slack state (its weight is "slack").
+ * lb/ub: nu + nx bounds in z order [u x] (model_map.yaml columns 3, 4).
  * Options take the defaults listed in mpcg_problem.  Returns 0, or -1 with
  * mpcg_last_error() naming the missing entry. */
-int mpcg_problem_from_map(mpcg_problem *pr, int N, int npar, int n_entries, const char *const *names,
+int mpcg_problem_from_map(mpcg_problem *pr, int N, int nx, int npar, int n_entries, const char *const *names,
                           const int *indices, const double *lb, const double *ub, double dt,
                           int sqp_iters);
 
@@ -147,7 +157,7 @@ typedef struct mpcg_scene_io {
  * [S*G][N][npar], warm [S*G][N+1][nvar], xinit [S*G][nx] (the mpcg_io inputs),
  * prev_interp [S][N][2] (the consistency reference, may be NULL) and
  * consistency_active [S*G] (may be NULL), enqueued on `stream`.  Requires
- * N <= 32 and min(n_lin, n_ell) <= 24.  Returns 0 on a successful launch. */
+ * nx 5 (the T-MPC problem), N <= 32 and min(n_lin, n_ell) <= 24.  Returns 0 on a successful launch. */
 int mpcg_prepare(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg_scene_io *in,
                  double *params, double *warm, double *xinit, double *prev_interp,
                  unsigned char *consistency_active, void *stream);
@@ -189,7 +199,7 @@ int mpcg_advance(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg
                  unsigned char *consistency_on_next, unsigned char *previously_selected_next, double *lam_next,
                  void *stream);
 
-/* 0 if (N, n_lin, n_ell) has a compiled kernel instance, else -1 */
+/* 0 if (N, nx, n_lin, n_ell, n_scen) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);
 
 /* Batched solve, every pointer in device memory, enqueued on `stream`

@@ -157,7 +157,8 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
     if (N != SOLVER_N || (int)npar != SOLVER_NP || (int)nx != SOLVER_NX || (int)nu != SOLVER_NU)
         fatal("solver_settings.yaml (N=" + std::to_string(N) + ", npar=" + std::to_string(npar) +
               ") does not match the compiled dimensions in mpcg_solver_dims.h");
-    if (nx != MPCG_NX || nu != MPCG_NU) fatal("the MI355X backend implements the 5-state unicycle model");
+    if ((nx != 5 && nx != 6) || nu != MPCG_NU)
+        fatal("the MI355X backend implements the contouring unicycle model (nx 5, or 6 with the slack state)");
 
     const mpcg::YamlNode& cfg = SolverConfig::settings();
     dt = cfg["integrator_step"].as<double>();
@@ -182,12 +183,13 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
         lb[i] = it->second[2].as<double>();
         ub[i] = it->second[3].as<double>();
     }
-    if (mpcg_problem_from_map(&_problem, N, npar, (int)names.size(), cnames.data(), idx.data(), lb.data(), ub.data(),
+    if (mpcg_problem_from_map(&_problem, N, (int)nx, npar, (int)names.size(), cnames.data(), idx.data(), lb.data(), ub.data(),
                               dt, _num_iterations) != 0)
         fatal(std::string("parameter map: ") + mpcg_last_error());
     if (mpcg_supported(&_problem) != 0)
-        fatal("no compiled kernel instance for N=" + std::to_string(N) + " with " + std::to_string(_problem.n_lin) +
-              " halfspaces and " + std::to_string(_problem.n_ell) + " obstacles");
+        fatal("no compiled kernel instance for N=" + std::to_string(N) + ", nx=" + std::to_string(nx) + " with " +
+              std::to_string(_problem.n_lin) + " halfspaces, " + std::to_string(_problem.n_ell) + " obstacles and " +
+              std::to_string(_problem.n_scen) + " scenario halfspaces");
     _iterate.assign((size_t)(N + 1) * nvar, 0.0);
     _lam.assign((size_t)mpcg_lam_size(&_problem), 0.0);
     reset();

@@ -6,6 +6,8 @@
 //                contouring.py:140-174 (stage_idx=1), consistency_module.py:229-250,
 //                glued spline spline.py:28-86
 //   constraints  guidance_constraints.py:355-370 then ellipsoid_constraints.py:435-489
+//   slack model  solver_model.py:274-298 (slack state last, constant in time),
+//                its MPCBase weight slack^2 (generate_jackalsimulator_solver.py:69-89)
 //   dynamics     solver_model.py:207-214 integrated by acados ERK (4 stages,
 //                3 steps) with exact first/second-order sensitivities
 //                (generate_acados_solver.py:148-157)
@@ -17,7 +19,7 @@
 
 namespace mpcg {
 
-constexpr int NX = MPCG_NX, NU = MPCG_NU, NZ = MPCG_NVAR;
+constexpr int NU = MPCG_NU;
 
 // ---------------------------------------------------------------------------
 // fp64 reciprocal / reciprocal square root: the hardware estimate
@@ -112,10 +114,13 @@ __device__ inline void spline_jets(const mpcg_problem& pr, const double* __restr
 }
 
 // ---------------------------------------------------------------------------
-// stage cost L(z; p), gradient and Hessian (z = [a, w, x, y, psi, v, s])
+// stage cost L(z; p), gradient and Hessian (z = [a, w, x, y, psi, v, s (, slack)])
 // ---------------------------------------------------------------------------
+template <int NX>
 __device__ inline double stage_cost(const mpcg_problem& pr, const double* __restrict__ p,
-                                    const double z[NZ], double g[NZ], double H[NZ][NZ], bool derivs) {
+                                    const double z[NU + NX], double g[NU + NX], double H[NU + NX][NU + NX],
+                                    bool derivs) {
+    constexpr int NZ = NU + NX;
     const double a = z[0], w = z[1], x = z[2], y = z[3], v = z[5], s = z[6];
     const double wa = p[pr.i_w_acc], ww = p[pr.i_w_ang], wv = p[pr.i_w_vel], vref = p[pr.i_v_ref];
     const double wc = p[pr.i_w_contour], wl = p[pr.i_w_lag];
@@ -135,6 +140,12 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
         dxp = x - p[pr.i_prev_x];
         dyp = y - p[pr.i_prev_y];
         L += wcn * (dxp * dxp + dyp * dyp);
+    }
+    double wsl = 0.0, sl = 0.0;
+    if constexpr (NX > 5) {
+        wsl = p[pr.i_w_slack];
+        sl = z[NU + 5];
+        L += wsl * sl * sl;
     }
     if (!derivs) return L;
     const double r1 = tx * J.Dx[1] + ty * J.Dy[1];
@@ -173,6 +184,10 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
         g[2] += 2.0 * wcn * dxp; g[3] += 2.0 * wcn * dyp;
         H[2][2] += 2.0 * wcn; H[3][3] += 2.0 * wcn;
     }
+    if constexpr (NX > 5) {
+        g[NU + 5] = 2.0 * wsl * sl;
+        H[NU + 5][NU + 5] = 2.0 * wsl;
+    }
     return L;
 }
 
@@ -184,10 +199,13 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
 //   x+ = x + sum_e h b_e v_e cos(psi_e), y+ likewise with sin, s+ = s + sum_e h b_e v_e,
 //   psi+ = psi + dt w, v+ = v + dt a,
 // and its exact Jacobian / second-order adjoint follow in closed form.
-// Outputs F = [B A] (5x7), xn, and (if pi != nullptr) H += Hess(pi' x+).
+// Outputs F = [B A] (nx x nz), xn, and (if pi != nullptr) H += Hess(pi' x+).
+// The slack state (nx 6) has zero dynamics: x+ = slack, a unit row.
 // ---------------------------------------------------------------------------
-__device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NZ], const double* pi,
-                                    double xn[NX], double F[NX][NZ], double H[NZ][NZ]) {
+template <int NX>
+__device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + NX], const double* pi,
+                                    double xn[NX], double F[NX][NU + NX], double H[NU + NX][NU + NX]) {
+    constexpr int NZ = NU + NX;
     const double a = z[0], w = z[1], psi = z[4], v = z[5];
     const int ns = pr.rk_steps;
     const double h = pr.dt / ns;
@@ -259,6 +277,11 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NZ], 
     F[0][2] = 1.0; F[1][3] = 1.0; F[4][6] = 1.0;
     F[2][1] = T; F[2][4] = 1.0;
     F[3][0] = T; F[3][5] = 1.0;
+#pragma unroll
+    for (int i = 5; i < NX; ++i) {
+        xn[i] = z[NU + i];
+        F[i][NU + i] = 1.0;
+    }
     if (pi) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -269,11 +292,12 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NZ], 
 
 // ---------------------------------------------------------------------------
 // MIRROR: H <- V f(D) V', f(d) = eps if |d| <= eps else |d|, cyclic Jacobi
-// on the 7x7 stage block.  Rotations on exactly-zero couplings are skipped,
+// on the nz x nz stage block.  Rotations on exactly-zero couplings are skipped,
 // so decoupled sub-blocks (e.g. {a,w,psi,v} vs {x,y,s} with a zero disc
 // offset) cost only their own rotations.
 // ---------------------------------------------------------------------------
-__device__ inline void mirror7(double A[NZ][NZ], double eps) {
+template <int NZ>
+__device__ inline void mirror(double A[NZ][NZ], double eps) {
     // Cyclic Jacobi on the symmetric part, one-sided rotation updates on the
     // upper triangle (a_pp -= t a_pq, a_qq += t a_pq, off-diagonal pairs with
     // tau = s / (1 + c)); V accumulates the eigenvectors.  Then

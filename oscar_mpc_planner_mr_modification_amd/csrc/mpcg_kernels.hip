@@ -9,7 +9,7 @@
 //   * stage lanes   lane k in [0, N]: linearisation of shooting stage k (cost,
 //                   ERK4 sensitivities + exact Hessian, constraints, MIRROR),
 //                   and every per-inequality interior-point operation of stage k
-//   * element lanes lane e < 49: one entry (i, j) of the 7x7 Riccati stage
+//   * element lanes lane e < nz (nz + 1) / 2: one entry (i >= j) of the Riccati stage
 //                   block during the backward factorisation
 //   * all lanes     redundant scalar recursions (vector pass, forward pass),
 //                   so no LDS round trip sits on those sequential chains
@@ -48,8 +48,8 @@ __global__ void select_best_kernel(int n_scenes, int G, int N, const double* __r
             // calculateConsistencyCostForSolver (guidance_constraints.cpp:1025-1050)
             double acc = 0.0;
             for (int k = 1; k <= N - 2; ++k) {
-                const double dx = xtraj[((size_t)s * (N + 1) + k) * NX + 0] - prev[((size_t)sc * N + k) * 2 + 0];
-                const double dy = xtraj[((size_t)s * (N + 1) + k) * NX + 1] - prev[((size_t)sc * N + k) * 2 + 1];
+                const double dx = xtraj[((size_t)s * (N + 1) + k) * MPCG_NX + 0] - prev[((size_t)sc * N + k) * 2 + 0];
+                const double dy = xtraj[((size_t)s * (N + 1) + k) * MPCG_NX + 1] - prev[((size_t)sc * N + k) * 2 + 1];
                 acc += dx * dx + dy * dy;
             }
             obj -= w_cons * acc;
@@ -84,12 +84,15 @@ using Fn = int (*)(const mpcg_problem&, int, const mpcg_io&, hipStream_t);
 
 static Fn find_instance(const mpcg_problem& pr) {
     if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return nullptr;
-#define MPCG_INST(N_, L_, E_) \
-    if (pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_) return &launch<Cfg<N_, L_, E_>>;
-    MPCG_INST(20, 4, 4)    // C1
-    MPCG_INST(20, 8, 8)    // C2 (north star)
-    MPCG_INST(30, 12, 12)  // C4
-    MPCG_INST(10, 2, 2)    // small test instance
+#define MPCG_INST(N_, L_, E_, S_, X_)                                                              \
+    if (pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_ && pr.n_scen == S_ && pr.nx == X_) \
+        return &launch<Cfg<N_, L_, E_, S_, X_>>;
+    MPCG_INST(20, 4, 4, 0, 5)    // C1
+    MPCG_INST(20, 8, 8, 0, 5)    // C2 (north star)
+    MPCG_INST(30, 12, 12, 0, 5)  // C4
+    MPCG_INST(20, 0, 0, 24, 6)   // C5 (SH-MPC, slack model)
+    MPCG_INST(10, 2, 2, 0, 5)    // small test instances
+    MPCG_INST(10, 0, 0, 4, 6)
 #undef MPCG_INST
     return nullptr;
 }
@@ -98,8 +101,9 @@ static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
     if (!pr || batch < 0) { g_err = "invalid arguments"; return -1; }
     *fn = find_instance(*pr);
     if (!*fn) {
-        g_err = "no compiled instance for N=" + std::to_string(pr->N) + " n_lin=" + std::to_string(pr->n_lin) +
-                " n_ell=" + std::to_string(pr->n_ell);
+        g_err = "no compiled instance for N=" + std::to_string(pr->N) + " nx=" + std::to_string(pr->nx) +
+                " n_lin=" + std::to_string(pr->n_lin) + " n_ell=" + std::to_string(pr->n_ell) +
+                " n_scen=" + std::to_string(pr->n_scen);
         return -2;
     }
     return 0;
@@ -131,13 +135,14 @@ const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }
 
 int mpcg_supported(const mpcg_problem* pr) { return (pr && mpcg::find_instance(*pr)) ? 0 : -1; }
 
-int mpcg_num_h(const mpcg_problem* pr) { return pr ? pr->n_lin + pr->n_ell : 0; }
+int mpcg_num_h(const mpcg_problem* pr) { return pr ? pr->n_lin + pr->n_ell + pr->n_scen : 0; }
 
-int mpcg_lam_size(const mpcg_problem* pr) { return pr ? pr->N * (MPCG_NX + mpcg_num_h(pr)) : 0; }
+int mpcg_lam_size(const mpcg_problem* pr) { return pr ? pr->N * (pr->nx + mpcg_num_h(pr)) : 0; }
 
-int mpcg_problem_from_map(mpcg_problem* pr, int N, int npar, int n_entries, const char* const* names,
+int mpcg_problem_from_map(mpcg_problem* pr, int N, int nx, int npar, int n_entries, const char* const* names,
                           const int* indices, const double* lb, const double* ub, double dt, int sqp_iters) {
-    if (!pr || !names || !indices || !lb || !ub || N < 1 || npar < 1 || n_entries < 0) {
+    if (!pr || !names || !indices || !lb || !ub || N < 1 || npar < 1 || n_entries < 0 || nx < 5 ||
+        nx > MPCG_MAX_NX) {
         mpcg::g_err = "invalid arguments";
         return -1;
     }
@@ -148,6 +153,7 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int npar, int n_entries, cons
     };
     std::memset(pr, 0, sizeof(*pr));
     pr->N = N;
+    pr->nx = nx;
     pr->npar = npar;
     // MPCBase weights (mpc_base.py:47-60), contouring (contouring.py:114-138)
     pr->i_w_acc = find("acceleration");
@@ -166,13 +172,19 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int npar, int n_entries, cons
     pr->i_disc_off = find("ego_disc_0_offset");
     pr->i_lin0 = find("lin_constraint_0_a1");
     pr->i_ell0 = find("ellipsoid_obst_0_x");
+    // scenario halfspaces (scenario_constraints.py:41-50) and the slack weight
+    pr->i_scen0 = find("disc_0_scenario_constraint_0_a1");
+    pr->i_w_slack = find("slack");
     const char* required[] = {"acceleration", "angular_velocity", "velocity", "reference_velocity", "contour",
-                              "lag", "spline_x0_a", "ego_disc_radius", "ego_disc_0_offset"};
+                              "lag", "spline_x0_a", "ego_disc_0_offset"};
     for (const char* r : required)
         if (find(r) < 0) { mpcg::g_err = std::string("parameter map has no '") + r + "'"; return -1; }
+    if (nx > 5 && pr->i_w_slack < 0) { mpcg::g_err = "parameter map has no 'slack'"; return -1; }
     while (find("spline" + std::to_string(pr->n_seg) + "_start") >= 0) ++pr->n_seg;
     while (find("lin_constraint_" + std::to_string(pr->n_lin) + "_a1") >= 0) ++pr->n_lin;
     while (find("ellipsoid_obst_" + std::to_string(pr->n_ell) + "_x") >= 0) ++pr->n_ell;
+    while (find("disc_0_scenario_constraint_" + std::to_string(pr->n_scen) + "_a1") >= 0) ++pr->n_scen;
+    if (pr->n_ell > 0 && pr->i_disc_r < 0) { mpcg::g_err = "parameter map has no 'ego_disc_radius'"; return -1; }
     // the kernels read bundles at fixed strides from their base index: check them
     for (int j = 0; j < pr->n_seg; ++j)
         if (find("spline_y" + std::to_string(j) + "_d") != pr->i_spline0 + 9 * j + 7 ||
@@ -190,10 +202,15 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int npar, int n_entries, cons
             mpcg::g_err = "obstacle " + std::to_string(j) + " is not contiguous";
             return -1;
         }
+    for (int i = 0; i < pr->n_scen; ++i)
+        if (find("disc_0_scenario_constraint_" + std::to_string(i) + "_b") != pr->i_scen0 + 3 * i + 2) {
+            mpcg::g_err = "scenario halfspace " + std::to_string(i) + " is not contiguous";
+            return -1;
+        }
     pr->dt = dt;
     pr->rk_steps = 3;  // sim_method_num_steps (generate_acados_solver.py:148-150)
     for (int i = 0; i < MPCG_NU; ++i) { pr->lbu[i] = lb[i]; pr->ubu[i] = ub[i]; }
-    for (int i = 0; i < MPCG_NX; ++i) { pr->lbx[i] = lb[MPCG_NU + i]; pr->ubx[i] = ub[MPCG_NU + i]; }
+    for (int i = 0; i < nx; ++i) { pr->lbx[i] = lb[MPCG_NU + i]; pr->ubx[i] = ub[MPCG_NU + i]; }
     pr->sqp_iters = sqp_iters;
     pr->qp_tol = 1e-5;
     pr->qp_iter_max = 50;
@@ -232,10 +249,11 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
     c->max_batch = max_batch;
     const size_t B = max_batch, N = pr->N;
     c->n_par = B * N * pr->npar;
-    c->n_warm = B * (N + 1) * MPCG_NVAR;
-    c->n_xi = B * MPCG_NX;
+    const size_t nx = pr->nx;
+    c->n_warm = B * (N + 1) * (MPCG_NU + nx);
+    c->n_xi = B * nx;
     c->n_lam = B * (size_t)mpcg_lam_size(pr);
-    c->n_xt = B * (N + 1) * MPCG_NX;
+    c->n_xt = B * (N + 1) * nx;
     c->n_ut = B * N * MPCG_NU;
     c->n_dbl = c->n_par + c->n_warm + c->n_xi + 2 * c->n_lam + c->n_xt + c->n_ut + B;
     c->n_int = B * (1 + MPCG_INFO_STRIDE);
@@ -280,8 +298,9 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
     if (batch == 0) return 0;
     const mpcg_problem& pr = c->pr;
     const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr);
-    const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * MPCG_NVAR, s_xi = B * MPCG_NX, s_lam = B * L;
-    const size_t s_xt = B * (N + 1) * MPCG_NX, s_ut = B * N * MPCG_NU;
+    const size_t nx = pr.nx;
+    const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * (MPCG_NU + nx), s_xi = B * nx, s_lam = B * L;
+    const size_t s_xt = B * (N + 1) * nx, s_ut = B * N * MPCG_NU;
     // inputs are packed contiguously (params | warm | xinit | lam_in) so one copy moves them
     double* h = c->host;
     std::memcpy(h, io->params, s_par * sizeof(double));

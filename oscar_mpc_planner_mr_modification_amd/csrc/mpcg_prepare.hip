@@ -23,6 +23,10 @@ int mpcg_prepare(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg
         mpcg::g_err = "mpcg_prepare: invalid arguments";
         return -1;
     }
+    if (pr->nx != MPCG_NX || pr->n_scen != 0) {
+        mpcg::g_err = "mpcg_prepare: the T-MPC producers need the 5-state model without scenario rows";
+        return -2;
+    }
     const int n_obs = pr->n_lin < pr->n_ell ? pr->n_lin : pr->n_ell;
     if (pr->N > mpcg::PREP_MAX_N || n_obs > mpcg::PREP_MAX_OBS || pr->N < 2) {
         mpcg::g_err = "mpcg_prepare: N or the obstacle count exceeds the kernel's limits";
@@ -47,6 +51,10 @@ int mpcg_advance(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg
         !consistency_on_next || !previously_selected_next) {
         mpcg::g_err = "mpcg_advance: invalid arguments";
         return -1;
+    }
+    if (pr->nx != MPCG_NX) {
+        mpcg::g_err = "mpcg_advance: the T-MPC step bookkeeping needs the 5-state model";
+        return -2;
     }
     if (n_scenes == 0) return 0;
     hipLaunchKernelGGL(mpcg::advance_kernel, dim3(n_scenes), dim3(64), 0, (hipStream_t)stream, *pr, n_scenes,

@@ -16,7 +16,7 @@
 // 1/t, residual, predictor product) in REGISTERS of its owner lane for the
 // whole QP; LDS holds only the stage blocks (~37 KB per solve for N=20 ->
 // 4 solves per CU, one wavefront per SIMD).
-//   element lanes      lane e < 28 owns entry (i >= j) of the 7x7 block in the
+//   element lanes      lane e < nz (nz + 1) / 2 owns entry (i >= j) of the nz x nz block in the
 //                      Riccati factorisation; the next stage's block is
 //                      prefetched while the current one is reduced
 //   chains             the two 5-vector recursions of each Newton solve run as
@@ -34,34 +34,55 @@ namespace mpcg {
 
 enum { AC_SUCCESS = 0, AC_NAN = 1, AC_MAXITER = 2, AC_MINSTEP = 3, AC_QP_FAILURE = 4 };
 
-constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
-
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int sym(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+// column-major packed lower triangle of an n x n block, a >= c
+__host__ __device__ constexpr int cpk(int n, int a, int c) { return c * n - c * (c - 1) / 2 + (a - c); }
 
-template <int N_, int NL_, int NE_>
+// N: horizon, NL / NE / NS: topology halfspaces, obstacle ellipsoids,
+// scenario halfspaces per stage, NX_: 5 (unicycle) or 6 (unicycle + slack)
+template <int N_, int NL_, int NE_, int NS_ = 0, int NX_ = 5>
 struct Cfg {
-    static constexpr int N = N_, NL = NL_, NE = NE_;
-    static constexpr int NH = NL + NE;
+    static constexpr int N = N_, NL = NL_, NE = NE_, NS = NS_;
+    static constexpr int NX = NX_, NZ = NU + NX_;
+    static_assert(NX == 5 || NX == 6, "unicycle model with or without the slack state");
+    static constexpr int NH = NL + NE + NS;
+    static constexpr int NTRI = NZ * (NZ + 1) / 2;  // packed stage block
+    static constexpr int NPT = NX * (NX + 1) / 2;   // packed cost-to-go
+    // h rows touch (x, y, psi) and, with the slack model, the slack state:
+    // the barrier block of the h rows is NB x NB on those variables
+    static constexpr int NB = (NX > 5 && NS > 0) ? 4 : 3;
+    static constexpr int NBT = NB * (NB + 1) / 2;
+    static constexpr int NDH = NZ + NBT + 1;         // dH: diag | block | zero slot
     static constexpr int PARTS = (64 / (N + 1)) >= 3 ? 3 : 2;
     static_assert((N + 1) * PARTS <= 64, "horizon too long for one wavefront");
+    static_assert(NTRI <= 64, "stage block larger than a wavefront");
     // rows of a lane: box slots j (variable part + PARTS j, lower and upper
     // side: slots 2j, 2j + 1), then h slots r (h row part + PARTS r)
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
+    static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
+    // block index of z variable v (-1: not touched by h rows)
+    __host__ __device__ static constexpr int blk(int v) {
+        return (v >= 2 && v <= 4) ? v - 2 : ((NB == 4 && v == NU + 5) ? 3 : -1);
+    }
+    // z variable of block index b
+    __host__ __device__ static constexpr int bvar(int b) { return b < 3 ? 2 + b : NU + 5; }
+    // slack coefficient of h row hh (scenario rows with the slack model)
+    __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
 
 template <class C>
 struct Lds {
-    static constexpr int N = C::N;
+    static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
     double z[N + 1][NZ];      // NLP iterate [u x]
-    double H[N + 1][28];      // MIRROR-regularised Lagrangian Hessian, packed lower triangle
+    double H[N + 1][C::NTRI]; // MIRROR-regularised Lagrangian Hessian, packed lower triangle
     double g[N + 1][NZ];
     double F[N][NX][NZ];      // [B A]
     double b[N][NX];          // shooting defects
-    double dH[N + 1][14];     // barrier terms: diag(7) + (x,y,psi) block packed xx xy xp yy yp pp, [13] = 0
+    double dH[N + 1][C::NDH]; // barrier terms: diag(nz) + h-row block (column-major packed), last = 0
     double q[N + 1][NZ];      // Newton gradient
     double dz[N + 1][NZ];     // QP iterate
     double ddz[N + 1][NZ];    // QP step
@@ -69,13 +90,13 @@ struct Lds {
     double piq[N][NX];
     double pin[N][NX];
     double rdyn[N][NX];
-    double P[N + 1][15];      // Riccati cost-to-go, packed
+    double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
     double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
     double Y[N][NU][NX];      // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
-    double Dg[N][C::NH][3];   // signed h-row gradients on (x, y, psi)
+    double Dg[N][C::NH][3];   // signed h-row gradients on (x, y, psi); the slack one is C::slack_coef
     double hd[N][C::NH];      // h-row bound gaps (uh - h or h - lh)
-    double Msc[28];           // factorisation scratch
+    double Msc[C::NTRI];      // factorisation scratch
     double xinit[NX];
     int flag;
 };
@@ -116,14 +137,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 
-// barrier contribution at (i, j), i >= j: diagonal part dh[0..6] plus the
-// (x, y, psi) block dh[7..12]
+// barrier contribution at (i, j), i >= j: diagonal part dh[0..nz) plus the
+// h-row block dh[nz..nz + NBT)
+template <class C>
 __device__ __forceinline__ double dh_at(const double* dh, int i, int j) {
     double v = (i == j) ? dh[i] : 0.0;
-    if (i >= 2 && i <= 4 && j >= 2 && j <= 4) {
-        const int a = i - 2, c = j - 2;
-        v += dh[NZ + ((c == 0) ? a : (c == 1 ? 2 + a : 5))];
-    }
+    const int a = C::blk(i), c = C::blk(j);
+    if (a >= 0 && c >= 0) v += dh[C::NZ + (a >= c ? cpk(C::NB, a, c) : cpk(C::NB, c, a))];
     return v;
 }
 
@@ -145,7 +165,7 @@ struct LaneRows {
     // input bounds on every stage < N, state bounds on 1..N-1
     __device__ __forceinline__ bool box_on(int j) const {
         const int v = var(j);
-        return v < NZ && (k == 0 ? v < NU : k < C::N);
+        return v < C::NZ && (k == 0 ? v < NU : k < C::N);
     }
     __device__ __forceinline__ bool h_on(int r) const { return k >= 1 && k < C::N && hrow(r) < C::NH; }
 };
@@ -153,11 +173,11 @@ struct LaneRows {
 // h values, signed gradients, bound gaps and the multiplier-weighted Hessian
 // (xx xy xp yy yp pp on x, y, psi) of the h rows of a lane at stage k.
 template <class C>
-__device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[NZ],
+__device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[C::NZ],
                                        const LaneRows<C>& LR, const double* nlam, double hb6[6], double (*Dg)[3],
                                        double* hd) {
     const double x = z[2], y = z[3], psi = z[4];
-    const double rdisc = pk[pr.i_disc_r], off = pk[pr.i_disc_off];
+    const double rdisc = C::NE > 0 ? pk[pr.i_disc_r] : 0.0, off = pk[pr.i_disc_off];
     double sp, cp;
     sincos(psi, &sp, &cp);
     const double dxp = -off * sp, dyp = off * cp, dxpp = -off * cp, dypp = -off * sp;
@@ -172,6 +192,17 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             Dg[hh][0] = c[0];
             Dg[hh][1] = c[1];
             Dg[hh][2] = 0.0;
+        } else if (hh >= C::NL + C::NE) {
+            // scenario halfspace a1 xd + a2 yd - (b + slack) <= 0 at the disc
+            // position (scenario_constraints.py:64-94)
+            const double* c = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
+            const double sl = C::NX > 5 ? z[NU + 5] : 0.0;
+            hd[hh] = 0.0 - (c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl));
+            Dg[hh][0] = c[0];
+            Dg[hh][1] = c[1];
+            Dg[hh][2] = c[0] * dxp + c[1] * dyp;
+            const double wgt = nlam[r];  // upper-bound row: Hessian weight +lambda
+            hb6[5] += wgt * (c[0] * dxpp + c[1] * dypp);
         } else {
             // obstacle ellipsoid d' R'DR d >= 1 (ellipsoid_constraints.py:435-489)
             const double* o = pk + pr.i_ell0 + 7 * (hh - C::NL);
@@ -206,7 +237,8 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
 template <class C>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps) {
-    constexpr int N = C::N, PARTS = C::PARTS;
+    constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
+    constexpr int ZS = NU + 5;  // slack variable (NB == 4)
     __shared__ Lds<C> S;
     const int sol = blockIdx.x;
     if (sol >= batch) return;
@@ -250,7 +282,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     if (lane < NX) S.xinit[lane] = io.xinit[(size_t)sol * NX + lane];
     for (int e = lane; e < N * NX; e += 64)
         (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
-    for (int e = lane; e <= N; e += 64) S.dH[e][13] = 0.0;
+    for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
     __syncthreads();
     if (lane < NU) S.z[N][lane] = 0.0;
     __syncthreads();
@@ -283,11 +315,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             double resl = 0.0;
             if (stage_lane && k < N) {
                 double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
-                stage_cost(pr, pk, zk, g, H, true);
+                stage_cost<NX>(pr, pk, zk, g, H, true);
                 STAMP_LAP(11);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
-                erk_unicycle(pr, zk, pi, xn, F, H);
+                erk_unicycle<NX>(pr, zk, pi, xn, F, H);
                 STAMP_LAP(12);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -304,7 +336,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
                 H[4][4] += hb6[5];
                 STAMP_LAP(13);
-                mirror7(H, pr.reg_eps);
+                mirror<NZ>(H, pr.reg_eps);
                 STAMP_LAP(14);
 #pragma unroll
                 for (int i = 0; i < NZ; ++i)
@@ -366,7 +398,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 double zk[NZ], dzk[NZ];
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) { dzk[i] = S.dz[ks][i]; zk[i] = S.z[ks][i]; }
-                double rh[3] = {0, 0, 0};
+                double rh[NB];
+#pragma unroll
+                for (int i = 0; i < NB; ++i) rh[i] = 0.0;
                 auto row_res = [&](int s, double ddot, double gap) {
                     const double l = R.l[s], t = R.t[s];
                     const double rin = ddot + t - gap;
@@ -393,19 +427,28 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     const int hh = LR.hrow(r);
                     const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2], l = R.l[HB + r];
                     rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;
-                    row_res(HB + r, a * dzk[2] + bq * dzk[3] + c * dzk[4], S.hd[k][hh]);
+                    double dd = a * dzk[2] + bq * dzk[3] + c * dzk[4];
+                    if constexpr (NB == 4) {
+                        const double sc = C::slack_coef(hh);
+                        rh[3] += sc * l;
+                        dd += sc * dzk[ZS];
+                    }
+                    row_res(HB + r, dd, S.hd[k][hh]);
                 }
-                double acc[3] = {rh[0], rh[1], rh[2]};
+                double acc[NB];
+#pragma unroll
+                for (int i = 0; i < NB; ++i) acc[i] = rh[i];
 #pragma unroll
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) acc[i] += __shfl_down(rh[i], p);
+                    for (int i = 0; i < NB; ++i) acc[i] += __shfl_down(rh[i], p);
                 __syncthreads();  // the owner lanes' box sums S.bx
                 if (stage_lane) {
                     double rbox[NZ];
 #pragma unroll
                     for (int i = 0; i < NZ; ++i) rbox[i] = S.bx[k][i];
-                    rbox[2] += acc[0]; rbox[3] += acc[1]; rbox[4] += acc[2];
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) rbox[C::bvar(i)] += acc[i];
                     double r[NZ];
 #pragma unroll
                     for (int i = 0; i < NZ; ++i) {
@@ -458,7 +501,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 // ---- barrier terms + Newton gradient
                 STAMP_BEGIN();
                 {
-                    double qh[3] = {0, 0, 0}, dbh[6] = {0, 0, 0, 0, 0, 0};
+                    double qh[NB], dbh[NBT];
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) qh[i] = 0.0;
+#pragma unroll
+                    for (int i = 0; i < NBT; ++i) dbh[i] = 0.0;
                     // coef = l + (l rin - rc) / t, wgt = l / t of slot s
                     auto bar = [&](int s, double& coef, double& wgt) {
                         const double l = R.l[s], t = R.t[s], itt = R.it[s];
@@ -487,33 +534,41 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const int hh = LR.hrow(r);
                         double coef, wgt;
                         bar(HB + r, coef, wgt);
-                        const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2];
-                        qh[0] += a * coef; qh[1] += bq * coef; qh[2] += c * coef;
+                        double dg[NB];
+                        dg[0] = S.Dg[k][hh][0]; dg[1] = S.Dg[k][hh][1]; dg[2] = S.Dg[k][hh][2];
+                        if constexpr (NB == 4) dg[3] = C::slack_coef(hh);
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) qh[i] += dg[i] * coef;
                         if (phase == 0) {
-                            dbh[0] += a * wgt * a; dbh[1] += a * wgt * bq; dbh[2] += a * wgt * c;
-                            dbh[3] += bq * wgt * bq; dbh[4] += bq * wgt * c; dbh[5] += c * wgt * c;
+#pragma unroll
+                            for (int c = 0; c < NB; ++c)
+#pragma unroll
+                                for (int a = c; a < NB; ++a) dbh[cpk(NB, a, c)] += dg[a] * wgt * dg[c];
                         }
                     }
-                    double aq[3] = {qh[0], qh[1], qh[2]}, ab[6];
+                    double aq[NB], ab[NBT];
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) ab[i] = dbh[i];
+                    for (int i = 0; i < NB; ++i) aq[i] = qh[i];
+#pragma unroll
+                    for (int i = 0; i < NBT; ++i) ab[i] = dbh[i];
 #pragma unroll
                     for (int p = 1; p < PARTS; ++p) {
 #pragma unroll
-                        for (int i = 0; i < 3; ++i) aq[i] += __shfl_down(qh[i], p);
+                        for (int i = 0; i < NB; ++i) aq[i] += __shfl_down(qh[i], p);
                         if (phase == 0) {
 #pragma unroll
-                            for (int i = 0; i < 6; ++i) ab[i] += __shfl_down(dbh[i], p);
+                            for (int i = 0; i < NBT; ++i) ab[i] += __shfl_down(dbh[i], p);
                         }
                     }
                     __syncthreads();  // the owner lanes' box sums S.bx
                     if (stage_lane) {
 #pragma unroll
                         for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[i] + S.g[k][i] + S.bx[k][i];
-                        S.q[k][2] += aq[0]; S.q[k][3] += aq[1]; S.q[k][4] += aq[2];
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) S.q[k][C::bvar(i)] += aq[i];
                         if (phase == 0) {
 #pragma unroll
-                            for (int i = 0; i < 6; ++i) S.dH[k][NZ + i] = ab[i];
+                            for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
                         }
                     }
                 }
@@ -522,35 +577,36 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 // ---- Riccati factorisation (predictor only; the corrector reuses it)
                 STAMP_BEGIN();
                 if (phase == 0) {
-                    // element lane -> (ei, ej), ei >= ej, of the 7x7 block
+                    constexpr int NT = C::NTRI, NP = C::NPT, DZ = C::NDH - 1;
+                    // element lane -> (ei, ej), ei >= ej, of the nz x nz block
                     int ei = 0;
-                    while ((ei + 1) * (ei + 2) / 2 <= lane && ei < 6) ++ei;
-                    const int ej = lane < 28 ? lane - ei * (ei + 1) / 2 : 0;
-                    // barrier entries of (ei, ej); 13 is the always-zero slot
-                    const int dhd = (ei == ej) ? ei : 13;
-                    int dhb = 13;
-                    if (ei >= 2 && ei <= 4 && ej >= 2 && ej <= 4) {
-                        const int a = ei - 2, c = ej - 2;
-                        dhb = NZ + ((c == 0) ? a : (c == 1 ? 2 + a : 5));
+                    while ((ei + 1) * (ei + 2) / 2 <= lane && ei < NZ - 1) ++ei;
+                    const int ej = lane < NT ? lane - ei * (ei + 1) / 2 : 0;
+                    // barrier entries of (ei, ej); DZ is the always-zero slot
+                    const int dhd = (ei == ej) ? ei : DZ;
+                    int dhb = DZ;
+                    {
+                        const int a = C::blk(ei), c = C::blk(ej);
+                        if (a >= 0 && c >= 0) dhb = NZ + (a >= c ? cpk(NB, a, c) : cpk(NB, c, a));
                     }
-                    // P lanes: (pi_, pj_) of the 5x5 block
+                    // P lanes: (pi_, pj_) of the nx x nx block
                     int pi_ = 0;
-                    while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < 4) ++pi_;
-                    const int pj_ = lane < 15 ? lane - pi_ * (pi_ + 1) / 2 : 0;
-                    if (lane < 15) S.P[N][lane] = S.H[N][sym(NU + pi_, NU + pj_)] + dh_at(S.dH[N], NU + pi_, NU + pj_);
+                    while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < NX - 1) ++pi_;
+                    const int pj_ = lane < NP ? lane - pi_ * (pi_ + 1) / 2 : 0;
+                    if (lane < NP) S.P[N][lane] = S.H[N][sym(NU + pi_, NU + pj_)] + dh_at<C>(S.dH[N], NU + pi_, NU + pj_);
                     if (lane == 0) S.flag = 0;
                     __syncthreads();
                     // prefetch of stage N-1's block
-                    const int le = lane < 28 ? lane : 0;
+                    const int le = lane < NT ? lane : 0;
                     double fi[NX], fj[NX], hv;
 #pragma unroll
                     for (int m = 0; m < NX; ++m) { fi[m] = S.F[N - 1][m][ei]; fj[m] = S.F[N - 1][m][ej]; }
                     hv = S.H[N - 1][le] + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
 #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
-                        double Pm[15];
+                        double Pm[NP];
 #pragma unroll
-                        for (int e = 0; e < 15; ++e) Pm[e] = S.P[kk + 1][e];
+                        for (int e = 0; e < NP; ++e) Pm[e] = S.P[kk + 1][e];
                         // prefetch the next (lower) stage's block; it lands while this one is reduced
                         const int kn = kk > 0 ? kk - 1 : 0;
                         double fi2[NX], fj2[NX];
@@ -565,14 +621,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
                             v += fi[m] * tm;
                         }
-                        if (lane < 28) S.Msc[lane] = v;
+                        if (lane < NT) S.Msc[lane] = v;
 #pragma unroll
                         for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
                         hv = hv2;
                         STAMP_LAP(16);
                         __syncthreads();
                         STAMP_LAP(17);
-                        if (lane < 15) {
+                        if (lane < NP) {
                             const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
                             // 2x2 Cholesky through reciprocal square roots
                             const double il00 = frsq(m00);
@@ -659,16 +715,20 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
-                    const double ya = y0a + W0[0] * pmine[0] + W0[1] * pmine[1] + W0[2] * pmine[2] + W0[3] * pmine[3] +
-                                      W0[4] * pmine[4];
-                    const double yb = y0b + W1[0] * pmine[0] + W1[1] * pmine[1] + W1[2] * pmine[2] + W1[3] * pmine[3] +
-                                      W1[4] * pmine[4];
+                    double ya = y0a, yb = y0b;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        ya += W0[i] * pmine[i];
+                        yb += W1[i] * pmine[i];
+                    }
                     const double kf1 = -yb * il11;
                     const double kf0 = (-ya - l10 * kf1) * il00;
                     double e[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) e[i] = S.rdyn[kq][i] + S.F[kq][i][0] * kf0 + S.F[kq][i][1] * kf1;
-                    double dxu[NX] = {0, 0, 0, 0, 0}, dxmine[NX] = {0, 0, 0, 0, 0};
+                    double dxu[NX], dxmine[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) { dxu[i] = 0.0; dxmine[i] = 0.0; }
                     #pragma unroll
                     for (int kk = 0; kk < N; ++kk) {
                         double dn[NX];
@@ -737,7 +797,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     auto ddot = [&](int s) {
                         if (s < HB) return (s & 1) ? ddb[s >> 1] : -ddb[s >> 1];
                         const int hh = LR.hrow(s - HB);
-                        return S.Dg[k][hh][0] * ddk[2] + S.Dg[k][hh][1] * ddk[3] + S.Dg[k][hh][2] * ddk[4];
+                        double v = S.Dg[k][hh][0] * ddk[2] + S.Dg[k][hh][1] * ddk[3] + S.Dg[k][hh][2] * ddk[4];
+                        if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
+                        return v;
                     };
                     auto active = [&](int s) { return s < HB ? LR.box_on(s >> 1) : LR.h_on(s - HB); };
                     // dt = -rin - D ddz; dl = -(rc + l dt) / t
@@ -842,7 +904,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         double zz[NZ], gd[NZ], Hd[NZ][NZ];
 #pragma unroll
         for (int i = 0; i < NZ; ++i) zz[i] = S.z[k][i];
-        Lk = stage_cost(pr, pk, zz, gd, Hd, false);
+        Lk = stage_cost<NX>(pr, pk, zz, gd, Hd, false);
     }
     const double pobj = wave_sum(Lk);
     double* xo = io.xtraj + (size_t)sol * (N + 1) * NX;

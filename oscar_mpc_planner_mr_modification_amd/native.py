@@ -37,7 +37,7 @@ def _load():
     lib.mpcg_supported.restype = C.c_int
     lib.mpcg_num_h.argtypes = [P]
     lib.mpcg_lam_size.argtypes = [P]
-    lib.mpcg_problem_from_map.argtypes = [P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_char_p),
+    lib.mpcg_problem_from_map.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_char_p),
                                           C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.c_double, C.c_int]
     lib.mpcg_solve.argtypes = [P, C.c_int, C.POINTER(MpcgIo), vp]
@@ -79,27 +79,32 @@ def _check(rc, what):
         raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
 
 
+def lam_stride(pr: MpcgProblem) -> int:
+    """Doubles per stage of a multiplier block: nx + nh (include/mpcg.h, mpcg_io)."""
+    return pr.nx + pr.n_lin + pr.n_ell + pr.n_scen
+
+
 def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=None, lam_in=None,
                        lam_out=False):
     """Batched solve on device tensors (torch, float64, on the current HIP device).
-    params (B, N, npar), warm (B, N+1, 7), xinit (B, 5), optional lam_in
-    (B, N, 5 + nh) NLP multipliers carried over from the previous solve.
+    params (B, N, npar), warm (B, N+1, nu+nx), xinit (B, nx), optional lam_in
+    (B, N, nx + nh) NLP multipliers carried over from the previous solve.
     Returns a dict of device tensors (+ "lam" if lam_out); asynchronous on
     `stream` (torch.cuda stream or None = current)."""
     import torch
 
     B = params.shape[0]
-    N = pr.N
-    LS = NX + pr.n_lin + pr.n_ell
+    N, nx = pr.N, pr.nx
+    LS = lam_stride(pr)
     assert params.dtype == torch.float64 and params.is_cuda and params.is_contiguous()
     assert tuple(params.shape) == (B, N, pr.npar), (tuple(params.shape), (B, N, pr.npar))
-    assert tuple(warm.shape) == (B, N + 1, NVAR) and warm.is_contiguous() and warm.dtype == torch.float64
-    assert tuple(xinit.shape) == (B, NX) and xinit.is_contiguous() and xinit.dtype == torch.float64
+    assert tuple(warm.shape) == (B, N + 1, NU + nx) and warm.is_contiguous() and warm.dtype == torch.float64
+    assert tuple(xinit.shape) == (B, nx) and xinit.is_contiguous() and xinit.dtype == torch.float64
     if lam_in is not None:
         assert tuple(lam_in.shape) == (B, N, LS) and lam_in.is_contiguous() and lam_in.dtype == torch.float64
     dev = params.device
     if out is None:
-        out = dict(xtraj=torch.empty((B, N + 1, NX), dtype=torch.float64, device=dev),
+        out = dict(xtraj=torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev),
                    utraj=torch.empty((B, N, NU), dtype=torch.float64, device=dev),
                    pobj=torch.empty((B,), dtype=torch.float64, device=dev),
                    exit=torch.empty((B,), dtype=torch.int32, device=dev),
@@ -144,13 +149,13 @@ class Context:
 
     def solve(self, params, warm, xinit, lam_in=None, lam_out=False):
         pr = self.pr
-        B, N = params.shape[0], pr.N
-        LS = NX + pr.n_lin + pr.n_ell
+        B, N, nx = params.shape[0], pr.N, pr.nx
+        LS = lam_stride(pr)
         params = np.ascontiguousarray(params, np.float64)
         warm = np.ascontiguousarray(warm, np.float64)
         xinit = np.ascontiguousarray(xinit, np.float64)
-        assert params.shape == (B, N, pr.npar) and warm.shape == (B, N + 1, NVAR) and xinit.shape == (B, NX)
-        r = dict(xtraj=np.zeros((B, N + 1, NX)), utraj=np.zeros((B, N, NU)), pobj=np.zeros(B),
+        assert params.shape == (B, N, pr.npar) and warm.shape == (B, N + 1, NU + nx) and xinit.shape == (B, nx)
+        r = dict(xtraj=np.zeros((B, N + 1, nx)), utraj=np.zeros((B, N, NU)), pobj=np.zeros(B),
                  exit=np.zeros(B, np.int32), info=np.zeros((B, INFO_STRIDE), np.int32))
         if lam_in is not None:
             lam_in = np.ascontiguousarray(lam_in, np.float64)
@@ -167,12 +172,12 @@ class Context:
 def solve_batch_host(pr: MpcgProblem, params: np.ndarray, warm: np.ndarray, xinit: np.ndarray):
     """Host-buffer solve through the same kernels (copies in/out, synchronous)."""
     B = params.shape[0]
-    N = pr.N
+    N, nx = pr.N, pr.nx
     params = np.ascontiguousarray(params, np.float64)
     warm = np.ascontiguousarray(warm, np.float64)
     xinit = np.ascontiguousarray(xinit, np.float64)
-    assert params.shape == (B, N, pr.npar) and warm.shape == (B, N + 1, NVAR) and xinit.shape == (B, NX)
-    xt = np.zeros((B, N + 1, NX))
+    assert params.shape == (B, N, pr.npar) and warm.shape == (B, N + 1, NU + nx) and xinit.shape == (B, nx)
+    xt = np.zeros((B, N + 1, nx))
     ut = np.zeros((B, N, NU))
     po = np.zeros(B)
     ex = np.zeros(B, np.int32)
@@ -254,7 +259,7 @@ def advance_device(pr: MpcgProblem, S: int, G: int, best, exit_code, xtraj, utra
 
     dev = xtraj.device
     N = pr.N
-    LS = NX + pr.n_lin + pr.n_ell
+    LS = lam_stride(pr)
     out = dict(main_warm=torch.empty((S, N + 1, NVAR), dtype=torch.float64, device=dev),
                prev_traj=torch.empty((S, N, 2), dtype=torch.float64, device=dev),
                prev_elapsed=torch.empty((S,), dtype=torch.float64, device=dev),

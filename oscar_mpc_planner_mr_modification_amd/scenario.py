@@ -1,0 +1,158 @@
+"""SH-MPC (configuration_safe_horizon) solver inputs.
+
+The reference's ScenarioConstraints module (scenario_constraints.cpp:58-110)
+runs `parallel_solvers` (4, settings.yaml:48-49) copies of the main solver.
+Each copy draws its own obstacle prediction samples
+(onDataReceived -> IntegrateAndTranslateToMeanAndVariance, :112-131), reduces
+them to 24 halfspaces per stage in the external `scenario_module`, writes them
+as `disc_0_scenario_constraint_<i>_{a1,a2,b}` and solves; the lowest-cost
+successful copy wins (:86-103).  The solve itself is the same batched
+SQP-RTI path on the slack model (ContouringSecondOrderUnicycleModelWithSlack,
+solver_model.py:274-298): one batch element per (scene, parallel solver).
+
+`scenario_module` is not part of the reference, so the sample -> halfspace
+reduction here is a restatement of its published idea, PARITY UNPINNED:
+  samples   per obstacle, a Gaussian random walk around the constant-velocity
+            mean (velocity noise integrated over the stages, so sample paths
+            are time-correlated like an integrated process-noise model);
+  halfspace for a sample q at stage k and the ego reference position p_k (the
+            warm start), n = (q - p_k) / |q - p_k|, n . p <= n . q - (r_robot + r_obs);
+  reduction keep the `n_constraints` halfspaces of the closest samples
+            (smallest |q - p_k|), closest first.
+Stage 0 carries inactive dummies (it is not part of the QP).
+
+Slack semantics on the reference's acados path: `ocp.constraints.x0` covers
+all nx states (generate_acados_solver.py:95), Solver::setXinit(State) writes
+the state's slack (0, state.cpp:20-23) and the slack has zero dynamics, so the
+slack stays at its initial value over the horizon and the scenario rows act
+as hard constraints; a copy whose halfspaces are contradictory ends in a QP
+failure, and the pick below takes another copy.
+
+Seeds: scene i uses `seed + i`; parallel solver s draws its samples from
+`seed + i` with stream s, so any sub-range regenerates bit-identically.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .layouts import Layout
+from .synthetic import DECELERATION, OBSTACLE_RADIUS, ROBOT_RADIUS, SETTINGS_WEIGHTS, _path, _path_eval
+
+SEED0 = 20251212
+SLACK_WEIGHT = 10000.0        # settings.yaml:89
+PARALLEL_SOLVERS = 4          # settings.yaml:48-49
+SAMPLE_VEL_STD = 0.3          # [m/s] per-axis velocity noise integrated over the horizon
+DUMMY_B = 100.0               # inactive stage-0 rows
+
+
+@dataclass
+class ScenarioBatch:
+    """Inputs of n_scenes * n_solvers independent solves, solve = scene * n_solvers + solver."""
+    params: np.ndarray   # (B*P, N, npar)
+    warm: np.ndarray     # (B*P, N+1, nu+nx)
+    xinit: np.ndarray    # (B*P, nx)
+    n_scenes: int
+    n_solvers: int
+
+
+def braking_warm(x0: np.ndarray, N: int, dt: float) -> np.ndarray:
+    """Solver::initializeWithBraking (acados_solver_interface.cpp:303-342) on
+    the slack model: the slack entries stay 0."""
+    warm = np.zeros((N + 1, 8))
+    x, y, psi, v, s = x0[:5]
+    a = -abs(DECELERATION)
+    warm[0, :7] = (a, 0.0, x, y, psi, v, s)
+    for k in range(1, N + 1):
+        x += v * dt * np.cos(psi)
+        y += v * dt * np.sin(psi)
+        s += v * dt
+        v = max(v + a * dt, 0.0)
+        warm[k, :7] = (a, 0.0, x, y, psi, v, s)
+    return warm
+
+
+def reduce_samples(samples: np.ndarray, ref: np.ndarray, n_constraints: int, radius: float) -> np.ndarray:
+    """samples (M, 2) at one stage, ref (2,) ego reference position ->
+    (n_constraints, 3) rows a1 a2 b of the closest samples, closest first."""
+    d = samples - ref[None, :]
+    dist = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
+    order = np.argsort(dist, kind="stable")[:n_constraints]
+    dd, dn = d[order], dist[order]
+    n = dd / np.maximum(dn, 1e-9)[:, None]
+    b = n[:, 0] * samples[order, 0] + n[:, 1] * samples[order, 1] - radius
+    out = np.zeros((n_constraints, 3))
+    out[:len(order), 0:2] = n
+    out[:len(order), 2] = b
+    return out
+
+
+def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
+                     n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioBatch:
+    assert layout.model == "unicycle_slack" and layout.n_scen > 0
+    N, dt, npar, ix = layout.N, layout.dt, layout.npar, layout.idx
+    nc = layout.n_scen
+    B, P = n_scenes, n_solvers
+    params = np.zeros((B * P, N, npar))
+    warm = np.zeros((B * P, N + 1, 8))
+    xinit = np.zeros((B * P, 6))
+    i_scen = ix("disc_0_scenario_constraint_0_a1")
+    tk = dt * np.arange(N)
+    for sc in range(B):
+        rng = np.random.default_rng(seed + first_scene + sc)
+        coef, starts = _path(rng, layout.n_seg)
+        s_ego = rng.uniform(0.0, 1.0)
+        p_on, t_on = _path_eval(coef, starts, s_ego)
+        n_on = np.array([-t_on[1], t_on[0]])
+        ego_pos = p_on + rng.normal(0, 0.2) * n_on
+        v0 = rng.uniform(0.0, 2.0)
+        psi0 = np.arctan2(t_on[1], t_on[0]) + rng.normal(0.0, 0.1)
+        x0 = np.array([ego_pos[0], ego_pos[1], psi0, v0, s_ego, 0.0])
+        means = np.zeros((n_obs, N, 2))
+        for j in range(n_obs):
+            ahead = rng.uniform(2.0, 10.0)
+            lat = rng.uniform(-3.0, 3.0)
+            pj, tj = _path_eval(coef, starts, s_ego + ahead)
+            nj = np.array([-tj[1], tj[0]])
+            vj = rng.normal(0.0, 0.7, size=2)
+            means[j] = (pj + lat * nj)[None, :] + vj[None, :] * tk[:, None]
+        base = np.zeros(npar)
+        for name in ("acceleration", "angular_velocity", "velocity", "reference_velocity", "contour", "lag",
+                     "terminal_angle", "terminal_contouring"):
+            base[ix(name)] = SETTINGS_WEIGHTS[name]
+        base[ix("slack")] = SLACK_WEIGHT
+        for j in range(layout.n_seg):
+            for ax, axn in enumerate("xy"):
+                for ci, cn in enumerate("abcd"):
+                    base[ix(f"spline_{axn}{j}_{cn}")] = coef[j, ax, ci]
+            base[ix(f"spline{j}_start")] = starts[j]
+        base[ix("ego_disc_0_offset")] = 0.0
+        w = braking_warm(x0, N, dt)
+        for s in range(P):
+            b = sc * P + s
+            srng = np.random.default_rng([seed + first_scene + sc, s + 1])
+            # (n_obs, n_samples, N, 2): integrated velocity noise, zero at stage 0
+            vel = srng.normal(0.0, SAMPLE_VEL_STD, size=(n_obs, n_samples, N, 2))
+            vel[:, :, 0] = 0.0
+            walk = np.cumsum(vel * dt, axis=2)
+            samples = means[:, None] + walk
+            params[b] = base[None, :]
+            rows = params[b, :, i_scen:i_scen + 3 * nc].reshape(N, nc, 3)
+            rows[0] = (0.0, 0.0, DUMMY_B)
+            for k in range(1, N):
+                rows[k] = reduce_samples(samples[:, :, k].reshape(-1, 2), w[k, 2:4], nc,
+                                         ROBOT_RADIUS + OBSTACLE_RADIUS)
+            warm[b] = w
+            xinit[b] = x0
+    return ScenarioBatch(params=params, warm=warm, xinit=xinit, n_scenes=B, n_solvers=P)
+
+
+def select_lowest_cost(pobj: np.ndarray, exit_code: np.ndarray, n_solvers: int) -> np.ndarray:
+    """ScenarioConstraints::optimize's pick (scenario_constraints.cpp:86-103):
+    the successful copy with the lowest pobj below 1e9; -1 when none."""
+    po = pobj.reshape(-1, n_solvers)
+    ok = (exit_code.reshape(-1, n_solvers) == 1) & (po < 1e9)
+    masked = np.where(ok, po, np.inf)
+    best = np.argmin(masked, axis=1)
+    return np.where(ok.any(axis=1), best, -1).astype(np.int32)

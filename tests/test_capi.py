@@ -51,13 +51,20 @@ def test_host_only_queries(lib):
     from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
     from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
     lib.mpcg_abi_version.restype = C.c_int
-    assert lib.mpcg_abi_version() == 2
-    for cfg in ("C1", "C2", "C4"):
+    assert lib.mpcg_abi_version() == 3
+    for cfg in ("C1", "C2", "C4", "C5"):
         pr = problem_from_layout(config_layout(cfg))
         assert lib.mpcg_supported(C.byref(pr)) == 0, cfg
     pr = problem_from_layout(config_layout("C2"))
     pr.N = 17
     assert lib.mpcg_supported(C.byref(pr)) == -1
+    pr = problem_from_layout(config_layout("C5"))
+    pr.nx = 5   # scenario rows on the model without the slack state: not compiled
+    assert lib.mpcg_supported(C.byref(pr)) == -1
+    lib.mpcg_num_h.restype = C.c_int
+    lib.mpcg_lam_size.restype = C.c_int
+    pr = problem_from_layout(config_layout("C5"))
+    assert lib.mpcg_num_h(C.byref(pr)) == 24 and lib.mpcg_lam_size(C.byref(pr)) == 20 * (6 + 24)
 
 
 def test_struct_layout_matches_header():
@@ -89,21 +96,21 @@ def test_io_struct_layout_matches_header():
 
 
 def _problem_from_map(lib, lay, drop=None, dt=0.2, iters=10):
-    from oscar_mpc_planner_mr_modification_amd.native_spec import UNICYCLE_LB, UNICYCLE_UB, MpcgProblem
+    from oscar_mpc_planner_mr_modification_amd.native_spec import MpcgProblem
     items = [(k, v) for k, v in lay.pmap.items() if k != drop]
     names = (C.c_char_p * len(items))(*[k.encode() for k, _ in items])
     idx = (C.c_int * len(items))(*[v for _, v in items])
-    lb = (C.c_double * 7)(*UNICYCLE_LB)
-    ub = (C.c_double * 7)(*UNICYCLE_UB)
+    lb = (C.c_double * lay.nvar)(*lay.lb)
+    ub = (C.c_double * lay.nvar)(*lay.ub)
     pr = MpcgProblem()
     lib.mpcg_problem_from_map.restype = C.c_int
     lib.mpcg_last_error.restype = C.c_char_p
-    rc = lib.mpcg_problem_from_map(C.byref(pr), lay.N, lay.npar, len(items), names, idx, lb, ub,
+    rc = lib.mpcg_problem_from_map(C.byref(pr), lay.N, lay.nx, lay.npar, len(items), names, idx, lb, ub,
                                    C.c_double(dt), iters)
     return rc, pr
 
 
-@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4", "C5"])
 def test_problem_from_parameter_map_matches_layout(lib, cfg):
     """mpcg_problem_from_map (what the C++ Solver calls on parameter_map.yaml)
     reproduces the Python layout's problem field by field."""
