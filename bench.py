@@ -21,6 +21,12 @@ with SURVEY.md §8(d)'s algorithmic bytes per solve (the path is fp64-VALU /
 latency bound); `cpu_baseline` times the C oracle (same
 algorithm, OpenMP over solves) on a bounded sample of the same batch, and
 `parity` is max |x - x_ref| over that sample.
+
+`--config C5` runs the SH-MPC workload instead: 2048
+scenes x 4 parallel scenario solvers per GPU on the slack model, 24 scenario
+halfspaces per stage reduced on the GPU from 12 obstacles x 100 prediction
+samples (mpcg_prepare_scenario), batched solve, lowest-cost pick
+(ScenarioConstraints::optimize) and the winner gather.
 """
 import argparse
 import json
@@ -50,7 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
-    ap.add_argument("--scenes", type=int, default=1024, help="scenes per GPU")
+    ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2/C4: 1024, C5: 2048)")
     ap.add_argument("--guesses", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -78,7 +84,9 @@ def main():
                                                                  concat_scenes, make_scenes)
 
     lay = config_layout(args.config)
-    S, G, N = args.scenes, args.guesses, lay.N
+    if args.config == "C5":
+        return run_shmpc(args, lay, world, rank, dev)
+    S, G, N = args.scenes or 1024, args.guesses, lay.N
     B = S * G
     W_CONS, SEL_W = SETTINGS_WEIGHTS["consistency"], 0.75   # guidance_planner.yaml:37 selection weight
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -234,6 +242,171 @@ def main():
                                             f"(same algorithm), OpenMP {threads} threads",
                                   "single_thread_solves_per_s": round(r1, 2),
                                   "eight_thread_solves_per_s": None if r8 is None else round(r8, 2)}
+        result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
+                            "solves_compared": compared, "tolerance": 1e-4}
+        result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_shmpc(args, lay, world, rank, dev):
+    """C5: SH-MPC step = scenario producer (samples -> halfspaces) + solve + lowest-cost pick + gather."""
+    import torch
+    import torch.distributed as dist
+
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners, winner_records, winner_width
+    from oscar_mpc_planner_mr_modification_amd.scenario import (OBSTACLE_RADIUS, PARALLEL_SOLVERS, ROBOT_RADIUS,
+                                                                ScenarioScenes, make_shmpc_scenes,
+                                                                prepare_scenario_host)
+    from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION
+
+    S, P, N, nx = args.scenes or 2048, PARALLEL_SOLVERS, lay.N, lay.nx
+    B = S * P
+    n_obs, n_samples = 12, 100
+    radius = ROBOT_RADIUS + OBSTACLE_RADIUS
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    workers = min(threads, 16)
+    first = rank * S
+    if workers > 1 and S >= 2 * workers:
+        from concurrent.futures import ProcessPoolExecutor
+        chunks = [c for c in np.array_split(np.arange(S), workers) if len(c)]
+        with ProcessPoolExecutor(max_workers=workers) as ex:
+            parts = list(ex.map(make_shmpc_scenes, [lay] * len(chunks), [len(c) for c in chunks],
+                                [P] * len(chunks), [n_obs] * len(chunks), [n_samples] * len(chunks),
+                                [20251212] * len(chunks), [first + int(c[0]) for c in chunks]))
+        scenes = ScenarioScenes(stage_params=np.concatenate([q.stage_params for q in parts]),
+                                state=np.concatenate([q.state for q in parts]),
+                                samples=np.concatenate([q.samples for q in parts]), n_solvers=P)
+        del parts
+    else:
+        scenes = make_shmpc_scenes(lay, S, P, n_obs, n_samples, first_scene=first)
+    gen_s = time.time() - t0
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_sp, d_st, d_smp = t(scenes.stage_params), t(scenes.state), t(scenes.samples)
+    pr = native.problem_from_layout(lay)
+    prep = dict(params=torch.empty((B, N, lay.npar), dtype=torch.float64, device=dev),
+                warm=torch.empty((B, N + 1, lay.nvar), dtype=torch.float64, device=dev),
+                xinit=torch.empty((B, nx), dtype=torch.float64, device=dev))
+    out = dict(xtraj=torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev),
+               utraj=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+               pobj=torch.empty((B,), dtype=torch.float64, device=dev),
+               exit=torch.empty((B,), dtype=torch.int32, device=dev),
+               info=torch.empty((B, 4), dtype=torch.int32, device=dev))
+    best = torch.empty((S,), dtype=torch.int32, device=dev)
+    win_w = winner_width(N, nx)
+    winners = torch.empty((S, win_w), dtype=torch.float64, device=dev)
+    gathered = torch.empty((S * world, win_w), dtype=torch.float64, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        native.prepare_scenario_device(pr, P, d_sp, d_st, d_smp, radius, DECELERATION, out=prep, stream=stream)
+        if i is not None:
+            ev[i][1].record(stream)
+        native.solve_batch_device(pr, prep["params"], prep["warm"], prep["xinit"], out=out, stream=stream)
+        if i is not None:
+            ev[i][2].record(stream)
+        native.select_lowest_cost_device(S, P, out["pobj"], out["exit"], out=best, stream=stream)
+        winner_records(out["xtraj"], out["utraj"], out["pobj"], best, P, out=winners)
+        if world > 1:
+            gather_winners(winners, world, out=gathered)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    if world > 1:
+        te = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(te[0]), float(te[1])
+    value = args.steps * B * world / elapsed
+    exit_h, xt_h, info_h = out["exit"].cpu().numpy(), out["xtraj"].cpu().numpy(), out["info"].cpu().numpy()
+    best_h = best.cpu().numpy()
+    bps = algorithmic_bytes_per_solve(lay)
+    achieved = bps * B / (kern_ms * 1e-3) / 1e9
+    # the producer is the HBM-heavy kernel: every sample read once
+    prep_bytes = B * ((N - 1) * n_obs * n_samples * 16 + N * lay.npar * 8 + (N + 1) * lay.nvar * 8)
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("batch") == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded scenes, SURVEY.md §8d C5)",
+        "config": {"workload": f"C5: SH-MPC slack model, N={N}, {lay.n_scen} scenario halfspaces per stage from "
+                               f"{n_obs} obstacles x {n_samples} samples, {S} scenes x {P} parallel solvers per GPU, "
+                               f"10 SQP-RTI iterations",
+                   "scenes_per_gpu": S, "parallel_solvers": P, "N": N,
+                   "parallelism": f"scene-sharded x{world}" + (" + RCCL all-gather of winners" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sqp_kernel",
+                     "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps,
+                     "producer": {"kernel": "scenario_prepare_kernel", "kernel_ms": round(prep_ms, 4),
+                                  "algorithmic_gbs": round(prep_bytes / (prep_ms * 1e-3) / 1e9, 2),
+                                  "frac": prep_bytes / (prep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+        "solver_stats": {"success_frac": float((exit_h == 1).mean()), "scene_feasible_frac": float((best_h >= 0).mean()),
+                         "qp_iters_per_solve": float(info_h[:, 1].mean()), "scene_gen_s": round(gen_s, 2)},
+        "phases_ms": {"prepare": round(prep_ms, 4), "solve": round(kern_ms, 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        oracle_py.build()
+        orc = oracle_py.Oracle(lay)
+        done_sc, t_cpu, chunk = 0, 0.0, 64
+        max_abs_dx, agree, compared = 0.0, 0, 0
+        host_b = None
+        while done_sc < S and t_cpu < args.cpu_seconds:
+            sl = slice(done_sc, min(S, done_sc + chunk))
+            sub = ScenarioScenes(stage_params=scenes.stage_params[sl], state=scenes.state[sl],
+                                 samples=scenes.samples[sl.start * P:sl.stop * P], n_solvers=P)
+            hb = prepare_scenario_host(lay, sub, radius, DECELERATION)   # untimed: producer restatement
+            host_b = hb if host_b is None else host_b
+            tc = time.perf_counter()
+            ref = orc.solve_batch(hb.params, hb.warm, hb.xinit, nthreads=threads)
+            t_cpu += time.perf_counter() - tc
+            bs = slice(sl.start * P, sl.stop * P)
+            ok = (ref["status"] == 1) & (exit_h[bs] == 1)
+            if ok.any():
+                max_abs_dx = max(max_abs_dx, float(np.abs(xt_h[bs][ok] - ref["xtraj"][ok]).max()))
+            agree += int((ref["status"] == exit_h[bs]).sum())
+            compared += len(ref["status"])
+            done_sc = sl.stop
+        done = done_sc * P
+        tc = time.perf_counter()
+        n1 = min(64, len(host_b.params))
+        orc.solve_batch(host_b.params[:n1], host_b.warm[:n1], host_b.xinit[:n1], nthreads=1)
+        r1 = n1 / (time.perf_counter() - tc)
+        result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
+                                  "kind": "port",
+                                  "sample": f"first {done} of the {B} solves of this batch (host-restated producer, "
+                                            f"untimed), C oracle (same algorithm), OpenMP {threads} threads",
+                                  "single_thread_solves_per_s": round(r1, 2)}
         result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
                             "solves_compared": compared, "tolerance": 1e-4}
         result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)

@@ -162,6 +162,39 @@ int mpcg_prepare(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg
                  double *params, double *warm, double *xinit, double *prev_interp,
                  unsigned char *consistency_active, void *stream);
 
+/* SH-MPC inputs of one control step (ScenarioConstraints::optimize,
+ * scenario_constraints.cpp:58-84) for S scenes x P parallel solvers, device
+ * pointers.  Semantics: oscar_mpc_planner_mr_modification_amd/scenario.py.
+ *   stage_params [S][npar]           parameters written identically on every stage
+ *                                    (weights incl. "slack", spline segments, disc offset)
+ *   state        [S][nx]             ego state (xinit)
+ *   main_warm    [S][N+1][nu+nx]     the main solver's warm start, or NULL = braking plan
+ *   samples      [S*P][N][M][2]      obstacle prediction samples of every parallel solver at
+ *                                    every stage (M = obstacles x samples per obstacle)
+ * Each solver's scenario rows at stage k >= 1 are the halfspaces of its
+ * n_scen samples closest to the warm-start position p_k (ties: lower sample
+ * index): n = (q - p_k) / max(|q - p_k|, 1e-9), b = n . q - radius; stage 0
+ * rows are inactive (0, 0, 100).  This reduction restates the external
+ * scenario_module (parity unpinned). */
+typedef struct mpcg_scenario_io {
+    const double *stage_params, *state, *main_warm, *samples;
+    int n_samples;                 /* M, at most 2048 */
+    double radius;                 /* robot radius + obstacle radius */
+    double deceleration;           /* deceleration_at_infeasible (braking plan) */
+} mpcg_scenario_io;
+
+/* Outputs params [S*P][N][npar], warm [S*P][N+1][nu+nx], xinit [S*P][nx]
+ * (solve = scene * P + solver), enqueued on `stream`.  Requires n_scen in
+ * 1..32 and N <= 32.  Returns 0 on a successful launch. */
+int mpcg_prepare_scenario(const mpcg_problem *pr, int n_scenes, int n_solvers, const mpcg_scenario_io *in,
+                          double *params, double *warm, double *xinit, void *stream);
+
+/* ScenarioConstraints::optimize's pick (scenario_constraints.cpp:86-103): per
+ * scene the parallel solver with exit 1 and the lowest pobj below 1e9 (first
+ * index on ties), -1 when none.  pobj / exit_code [S*P], best [S], device. */
+int mpcg_select_lowest_cost_device(int n_scenes, int n_solvers, const double *pobj, const int *exit_code,
+                                   int *best, void *stream);
+
 /* Bookkeeping between two control steps of every scene: the state the
  * reference keeps in Planner / GuidanceConstraints / each LocalPlanner's
  * solver (device pointers; semantics restated in producers.advance_host).

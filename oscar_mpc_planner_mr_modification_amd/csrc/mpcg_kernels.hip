@@ -65,6 +65,23 @@ __global__ void select_best_kernel(int n_scenes, int G, int N, const double* __r
     best[sc] = best_i;
 }
 
+// ---- ScenarioConstraints::optimize's pick (scenario_constraints.cpp:86-103)
+__global__ void select_lowest_cost_kernel(int n_scenes, int P, const double* __restrict__ pobj,
+                                          const int* __restrict__ exit_code, int* __restrict__ best) {
+    const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sc >= n_scenes) return;
+    double lowest = 1e9;
+    int b = -1;
+    for (int s = 0; s < P; ++s) {
+        const int i = sc * P + s;
+        if (exit_code[i] == 1 && pobj[i] < lowest) {
+            lowest = pobj[i];
+            b = s;
+        }
+    }
+    best[sc] = b;
+}
+
 // ---- dispatch over compiled instances ------------------------------------
 thread_local std::string g_err;  // also set by mpcg_prepare.hip
 static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG_STAMPS builds only)
@@ -364,6 +381,24 @@ int mpcg_select_best_device(int n_scenes, int n_guesses, int N, const double* xt
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         mpcg::g_err = std::string("select_best launch: ") + hipGetErrorString(e);
+        return -1;
+    }
+    return 0;
+}
+
+int mpcg_select_lowest_cost_device(int n_scenes, int n_solvers, const double* pobj, const int* exit_code, int* best,
+                                   void* stream) {
+    if (n_scenes < 0 || n_solvers < 1 || (n_scenes > 0 && (!pobj || !exit_code || !best))) {
+        mpcg::g_err = "mpcg_select_lowest_cost_device: invalid arguments";
+        return -1;
+    }
+    if (n_scenes == 0) return 0;
+    const int T = 64;
+    hipLaunchKernelGGL(mpcg::select_lowest_cost_kernel, dim3((n_scenes + T - 1) / T), dim3(T), 0, (hipStream_t)stream,
+                       n_scenes, n_solvers, pobj, exit_code, best);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        mpcg::g_err = std::string("select_lowest_cost launch: ") + hipGetErrorString(e);
         return -1;
     }
     return 0;

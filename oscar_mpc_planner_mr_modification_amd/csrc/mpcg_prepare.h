@@ -316,3 +316,135 @@ __global__ __launch_bounds__(64) void advance_kernel(mpcg_problem pr, int n_scen
 }
 
 }  // namespace mpcg
+
+namespace mpcg {
+
+// ---------------------------------------------------------------------------
+// SH-MPC inputs of one control step (include/mpcg.h, mpcg_prepare_scenario):
+// ScenarioConstraints::optimize copies the main solver into every parallel
+// solver and writes each copy's scenario halfspaces before its solve
+// (scenario_constraints.cpp:58-84).  Host restatement and semantics:
+// scenario.py (prepare_scenario_host); the reduction of samples to halfspaces
+// restates the external scenario_module (parity unpinned there).
+//
+// One workgroup of 4 wavefronts per (scene, parallel solver):
+//   warm start   main warm start or the braking plan (acados_solver_interface.cpp:303-342)
+//   halfspaces   wave w reduces stages k = 1 + w, 5 + w, ...: each lane holds the distances
+//                of samples lane, lane + 64, ... to the warm-start position p_k in registers,
+//                then n_scen wave arg-min rounds (distance, then sample index: the stable
+//                order of the host's argsort) pick the closest samples; row
+//                n = (q - p_k) / max(|q - p_k|, 1e-9), b = n . q - radius
+//   stage 0      inactive rows (0, 0, 100)
+// then the N x npar parameter block is streamed out with coalesced stores.
+// Memory bound: every sample is read once (N-1 stages x M x 16 B per solve).
+// ---------------------------------------------------------------------------
+constexpr int SCEN_MAX_N = 32, SCEN_MAX_ROWS = 32, SCEN_PER_LANE = 32;  // M <= 64 * 32
+constexpr double SCEN_DUMMY_B = 100.0;
+
+struct ScenLds {
+    double warm[SCEN_MAX_N + 1][MPCG_NU + MPCG_MAX_NX];
+    double rows[SCEN_MAX_N][SCEN_MAX_ROWS][3];
+};
+
+__global__ __launch_bounds__(256) void scenario_prepare_kernel(mpcg_problem pr, int n_scenes, int P,
+                                                               mpcg_scenario_io in, double* __restrict__ params,
+                                                               double* __restrict__ warm,
+                                                               double* __restrict__ xinit) {
+    __shared__ ScenLds L;
+    const int sol = blockIdx.x;
+    const int sc = sol / P;
+    if (sc >= n_scenes) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = pr.N, npar = pr.npar, nx = pr.nx, NV = MPCG_NU + nx, NS = pr.n_scen, M = in.n_samples;
+    const double dt = pr.dt;
+    const double* st = in.state + (size_t)sc * nx;
+
+    // ---- warm start: the main solver's, or Solver::initializeWithBraking (other entries 0)
+    if (in.main_warm) {
+        const double* mw = in.main_warm + (size_t)sc * (N + 1) * NV;
+        for (int e = tid; e < (N + 1) * NV; e += 256) L.warm[e / NV][e % NV] = mw[e];
+    } else if (tid == 0) {
+        double x = st[0], y = st[1], psi = st[2], v = st[3], s = st[4];
+        const double a = -fabs(in.deceleration);
+        const double c = cos(psi), sn = sin(psi);
+        for (int k = 0; k <= N; ++k) {
+            if (k > 0) {
+                x = __dadd_rn(x, __dmul_rn(__dmul_rn(v, dt), c));
+                y = __dadd_rn(y, __dmul_rn(__dmul_rn(v, dt), sn));
+                s = __dadd_rn(s, __dmul_rn(v, dt));
+                v = fmax(__dadd_rn(v, __dmul_rn(a, dt)), 0.0);
+            }
+            double* w = L.warm[k];
+            w[0] = a; w[1] = 0.0; w[2] = x; w[3] = y; w[4] = psi; w[5] = v; w[6] = s;
+            for (int i = 7; i < NV; ++i) w[i] = 0.0;
+        }
+    }
+    __syncthreads();
+
+    // ---- sample -> halfspace reduction, one stage per wave at a time
+    const double INF = __longlong_as_double(0x7ff0000000000000LL);
+    for (int k = 1 + wave; k < N; k += 4) {
+        const double* q = in.samples + ((size_t)sol * N + k) * (size_t)M * 2;
+        const double rx = L.warm[k][2], ry = L.warm[k][3];
+        double dist[SCEN_PER_LANE];
+#pragma unroll
+        for (int j = 0; j < SCEN_PER_LANE; ++j) {
+            const int i = lane + 64 * j;
+            double d = INF;
+            if (i < M) d = norm2_rn(__dsub_rn(q[2 * i], rx), __dsub_rn(q[2 * i + 1], ry));
+            dist[j] = d;
+        }
+        for (int r = 0; r < NS; ++r) {
+            double bd = INF;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int j = 0; j < SCEN_PER_LANE; ++j)
+                if (dist[j] < bd) { bd = dist[j]; bi = lane + 64 * j; }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const double od = __shfl_xor(bd, o);
+                const int oi = __shfl_xor(bi, o);
+                if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+            }
+            const bool found = bi < M;
+            if (found && lane == (bi & 63)) {
+#pragma unroll
+                for (int j = 0; j < SCEN_PER_LANE; ++j)
+                    if (j == (bi >> 6)) dist[j] = INF;
+            }
+            if (lane == 0) {
+                double a1 = 0.0, a2 = 0.0, b = 0.0;
+                if (found) {
+                    const double qx = q[2 * bi], qy = q[2 * bi + 1];
+                    const double dn = fmax(bd, 1e-9);
+                    a1 = __ddiv_rn(__dsub_rn(qx, rx), dn);
+                    a2 = __ddiv_rn(__dsub_rn(qy, ry), dn);
+                    b = __dsub_rn(__dadd_rn(__dmul_rn(a1, qx), __dmul_rn(a2, qy)), in.radius);
+                }
+                L.rows[k][r][0] = a1;
+                L.rows[k][r][1] = a2;
+                L.rows[k][r][2] = b;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- stream out the parameter block, warm start and xinit
+    const double* base = in.stage_params + (size_t)sc * npar;
+    double* Pp = params + (size_t)sol * N * npar;
+    const int s0 = pr.i_scen0;
+    for (int e = tid; e < N * npar; e += 256) {
+        const int k = e / npar, idx = e - k * npar;
+        double v = base[idx];
+        if (idx >= s0 && idx < s0 + 3 * NS) {
+            const int i = (idx - s0) / 3, c = (idx - s0) - 3 * i;
+            v = k == 0 ? (c == 2 ? SCEN_DUMMY_B : 0.0) : L.rows[k][i][c];
+        }
+        Pp[e] = v;
+    }
+    double* W = warm + (size_t)sol * (N + 1) * NV;
+    for (int e = tid; e < (N + 1) * NV; e += 256) W[e] = L.warm[e / NV][e % NV];
+    if (tid < nx) xinit[(size_t)sol * nx + tid] = st[tid];
+}
+
+}  // namespace mpcg

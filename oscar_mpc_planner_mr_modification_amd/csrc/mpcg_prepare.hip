@@ -68,4 +68,28 @@ int mpcg_advance(const mpcg_problem* pr, int n_scenes, int n_guesses, const mpcg
     return 0;
 }
 
+int mpcg_prepare_scenario(const mpcg_problem* pr, int n_scenes, int n_solvers, const mpcg_scenario_io* in,
+                          double* params, double* warm, double* xinit, void* stream) {
+    if (!pr || !in || n_scenes < 0 || n_solvers < 1 || !params || !warm || !xinit || !in->stage_params ||
+        !in->state || !in->samples) {
+        mpcg::g_err = "mpcg_prepare_scenario: invalid arguments";
+        return -1;
+    }
+    if (pr->n_scen < 1 || pr->i_scen0 < 0 || pr->nx < 5 || pr->nx > MPCG_MAX_NX || pr->N < 2 ||
+        pr->N > mpcg::SCEN_MAX_N || pr->n_scen > mpcg::SCEN_MAX_ROWS || in->n_samples < 1 ||
+        in->n_samples > 64 * mpcg::SCEN_PER_LANE) {
+        mpcg::g_err = "mpcg_prepare_scenario: needs scenario rows, N <= 32, n_scen <= 32 and 1..2048 samples";
+        return -2;
+    }
+    if (n_scenes == 0) return 0;
+    hipLaunchKernelGGL(mpcg::scenario_prepare_kernel, dim3(n_scenes * n_solvers), dim3(256), 0, (hipStream_t)stream,
+                       *pr, n_scenes, n_solvers, *in, params, warm, xinit);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        mpcg::g_err = std::string("scenario prepare launch: ") + hipGetErrorString(e);
+        return -1;
+    }
+    return 0;
+}
+
 }  // extern "C"

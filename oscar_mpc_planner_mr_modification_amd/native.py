@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX,  # noqa: F401
-                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, MpcgStepIo,
+                          UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, MpcgStepIo, MpcgScenarioIo,
                           problem_from_layout)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -58,6 +58,10 @@ def _load():
     lib.mpcg_prepare.restype = C.c_int
     lib.mpcg_advance.argtypes = [P, C.c_int, C.c_int, C.POINTER(MpcgStepIo), vp, vp, vp, vp, vp, vp, vp]
     lib.mpcg_advance.restype = C.c_int
+    lib.mpcg_prepare_scenario.argtypes = [P, C.c_int, C.c_int, C.POINTER(MpcgScenarioIo), vp, vp, vp, vp]
+    lib.mpcg_prepare_scenario.restype = C.c_int
+    lib.mpcg_select_lowest_cost_device.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp]
+    lib.mpcg_select_lowest_cost_device.restype = C.c_int
     if lib.mpcg_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
@@ -279,3 +283,44 @@ def advance_device(pr: MpcgProblem, S: int, G: int, best, exit_code, xtraj, utra
                           _ptr(out["lam"]), C.c_void_p(s.cuda_stream))
     _check(rc, "mpcg_advance")
     return out
+
+
+def prepare_scenario_device(pr: MpcgProblem, n_solvers: int, stage_params, state, samples, radius: float,
+                            deceleration: float, main_warm=None, out=None, stream=None):
+    """SH-MPC solver inputs on the GPU (mpcg_prepare_scenario): stage_params
+    (S, npar), state (S, nx), samples (S*P, N, M, 2), optional main_warm
+    (S, N+1, nu+nx) -> dict(params, warm, xinit) device tensors."""
+    import torch
+
+    S = stage_params.shape[0]
+    N, nx = pr.N, pr.nx
+    B = S * n_solvers
+    for t in (stage_params, state, samples) + (() if main_warm is None else (main_warm,)):
+        assert t.dtype == torch.float64 and t.is_cuda and t.is_contiguous()
+    assert tuple(state.shape) == (S, nx) and stage_params.shape[1] == pr.npar
+    assert samples.shape[0] == B and samples.shape[1] == N and samples.shape[3] == 2
+    dev = stage_params.device
+    if out is None:
+        out = dict(params=torch.empty((B, N, pr.npar), dtype=torch.float64, device=dev),
+                   warm=torch.empty((B, N + 1, NU + nx), dtype=torch.float64, device=dev),
+                   xinit=torch.empty((B, nx), dtype=torch.float64, device=dev))
+    io = MpcgScenarioIo(stage_params.data_ptr(), state.data_ptr(),
+                        None if main_warm is None else main_warm.data_ptr(), samples.data_ptr(),
+                        int(samples.shape[2]), float(radius), float(deceleration))
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    rc = lib.mpcg_prepare_scenario(C.byref(pr), S, n_solvers, C.byref(io), _ptr(out["params"]), _ptr(out["warm"]),
+                                   _ptr(out["xinit"]), C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_prepare_scenario")
+    return out
+
+
+def select_lowest_cost_device(n_scenes, n_solvers, pobj, exit_code, out=None, stream=None):
+    import torch
+
+    dev = pobj.device
+    best = out if out is not None else torch.empty((n_scenes,), dtype=torch.int32, device=dev)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    rc = lib.mpcg_select_lowest_cost_device(n_scenes, n_solvers, _ptr(pobj), _ptr(exit_code), _ptr(best),
+                                            C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_select_lowest_cost_device")
+    return best

@@ -96,9 +96,17 @@ class MpcgStepIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
+class MpcgScenarioIo(C.Structure):
+    """Mirror of `mpcg_scenario_io` (include/mpcg.h)."""
+    _fields_ = [("stage_params", C.c_void_p), ("state", C.c_void_p), ("main_warm", C.c_void_p),
+                ("samples", C.c_void_p), ("n_samples", C.c_int), ("radius", C.c_double),
+                ("deceleration", C.c_double)]
+
+
 ABI_VERSION = 3
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
            "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
-           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance")
+           "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
+           "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device")
 
 

@@ -48,6 +48,16 @@ DUMMY_B = 100.0               # inactive stage-0 rows
 
 
 @dataclass
+class ScenarioScenes:
+    """Scene-level SH-MPC inputs (the mpcg_scenario_io buffers, include/mpcg.h)."""
+    stage_params: np.ndarray  # (S, npar)
+    state: np.ndarray         # (S, nx)
+    samples: np.ndarray       # (S*P, N, M, 2), M = obstacles x samples per obstacle
+    n_solvers: int
+    main_warm: np.ndarray | None = None  # (S, N+1, nu+nx) or None = braking plan
+
+
+@dataclass
 class ScenarioBatch:
     """Inputs of n_scenes * n_solvers independent solves, solve = scene * n_solvers + solver."""
     params: np.ndarray   # (B*P, N, npar)
@@ -55,19 +65,21 @@ class ScenarioBatch:
     xinit: np.ndarray    # (B*P, nx)
     n_scenes: int
     n_solvers: int
+    scenes: ScenarioScenes | None = None
 
 
-def braking_warm(x0: np.ndarray, N: int, dt: float) -> np.ndarray:
-    """Solver::initializeWithBraking (acados_solver_interface.cpp:303-342) on
-    the slack model: the slack entries stay 0."""
-    warm = np.zeros((N + 1, 8))
-    x, y, psi, v, s = x0[:5]
-    a = -abs(DECELERATION)
+def braking_warm(x0: np.ndarray, N: int, dt: float, nvar: int = 8, decel: float = DECELERATION) -> np.ndarray:
+    """Solver::initializeWithBraking (acados_solver_interface.cpp:303-342); the
+    entries it does not write (the slack state) stay 0."""
+    warm = np.zeros((N + 1, nvar))
+    x, y, psi, v, s = (float(t) for t in x0[:5])
+    a = -abs(decel)
+    c, sn = np.cos(psi), np.sin(psi)
     warm[0, :7] = (a, 0.0, x, y, psi, v, s)
     for k in range(1, N + 1):
-        x += v * dt * np.cos(psi)
-        y += v * dt * np.sin(psi)
-        s += v * dt
+        x = x + v * dt * c
+        y = y + v * dt * sn
+        s = s + v * dt
         v = max(v + a * dt, 0.0)
         warm[k, :7] = (a, 0.0, x, y, psi, v, s)
     return warm
@@ -75,7 +87,8 @@ def braking_warm(x0: np.ndarray, N: int, dt: float) -> np.ndarray:
 
 def reduce_samples(samples: np.ndarray, ref: np.ndarray, n_constraints: int, radius: float) -> np.ndarray:
     """samples (M, 2) at one stage, ref (2,) ego reference position ->
-    (n_constraints, 3) rows a1 a2 b of the closest samples, closest first."""
+    (n_constraints, 3) rows a1 a2 b of the closest samples, closest first
+    (ties: lower sample index); rows past M stay 0."""
     d = samples - ref[None, :]
     dist = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
     order = np.argsort(dist, kind="stable")[:n_constraints]
@@ -88,18 +101,16 @@ def reduce_samples(samples: np.ndarray, ref: np.ndarray, n_constraints: int, rad
     return out
 
 
-def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
-                     n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioBatch:
+def make_shmpc_scenes(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
+                      n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioScenes:
     assert layout.model == "unicycle_slack" and layout.n_scen > 0
     N, dt, npar, ix = layout.N, layout.dt, layout.npar, layout.idx
-    nc = layout.n_scen
-    B, P = n_scenes, n_solvers
-    params = np.zeros((B * P, N, npar))
-    warm = np.zeros((B * P, N + 1, 8))
-    xinit = np.zeros((B * P, 6))
-    i_scen = ix("disc_0_scenario_constraint_0_a1")
+    S, P, M = n_scenes, n_solvers, n_obs * n_samples
+    stage_params = np.zeros((S, npar))
+    state = np.zeros((S, layout.nx))
+    samples = np.zeros((S * P, N, M, 2))
     tk = dt * np.arange(N)
-    for sc in range(B):
+    for sc in range(S):
         rng = np.random.default_rng(seed + first_scene + sc)
         coef, starts = _path(rng, layout.n_seg)
         s_ego = rng.uniform(0.0, 1.0)
@@ -108,7 +119,7 @@ def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SO
         ego_pos = p_on + rng.normal(0, 0.2) * n_on
         v0 = rng.uniform(0.0, 2.0)
         psi0 = np.arctan2(t_on[1], t_on[0]) + rng.normal(0.0, 0.1)
-        x0 = np.array([ego_pos[0], ego_pos[1], psi0, v0, s_ego, 0.0])
+        state[sc, :5] = (ego_pos[0], ego_pos[1], psi0, v0, s_ego)
         means = np.zeros((n_obs, N, 2))
         for j in range(n_obs):
             ahead = rng.uniform(2.0, 10.0)
@@ -117,7 +128,7 @@ def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SO
             nj = np.array([-tj[1], tj[0]])
             vj = rng.normal(0.0, 0.7, size=2)
             means[j] = (pj + lat * nj)[None, :] + vj[None, :] * tk[:, None]
-        base = np.zeros(npar)
+        base = stage_params[sc]
         for name in ("acceleration", "angular_velocity", "velocity", "reference_velocity", "contour", "lag",
                      "terminal_angle", "terminal_contouring"):
             base[ix(name)] = SETTINGS_WEIGHTS[name]
@@ -128,24 +139,47 @@ def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SO
                     base[ix(f"spline_{axn}{j}_{cn}")] = coef[j, ax, ci]
             base[ix(f"spline{j}_start")] = starts[j]
         base[ix("ego_disc_0_offset")] = 0.0
-        w = braking_warm(x0, N, dt)
         for s in range(P):
-            b = sc * P + s
             srng = np.random.default_rng([seed + first_scene + sc, s + 1])
             # (n_obs, n_samples, N, 2): integrated velocity noise, zero at stage 0
             vel = srng.normal(0.0, SAMPLE_VEL_STD, size=(n_obs, n_samples, N, 2))
             vel[:, :, 0] = 0.0
             walk = np.cumsum(vel * dt, axis=2)
-            samples = means[:, None] + walk
-            params[b] = base[None, :]
-            rows = params[b, :, i_scen:i_scen + 3 * nc].reshape(N, nc, 3)
+            smp = means[:, None] + walk                      # (n_obs, n_samples, N, 2)
+            samples[sc * P + s] = smp.transpose(2, 0, 1, 3).reshape(N, M, 2)
+    return ScenarioScenes(stage_params=stage_params, state=state, samples=samples, n_solvers=P)
+
+
+def prepare_scenario_host(layout: Layout, sc: ScenarioScenes, radius: float = ROBOT_RADIUS + OBSTACLE_RADIUS,
+                          deceleration: float = DECELERATION) -> ScenarioBatch:
+    """Host restatement of mpcg_prepare_scenario (include/mpcg.h): what
+    ScenarioConstraints::optimize writes into each parallel solver before its
+    solve (scenario_constraints.cpp:58-84)."""
+    N, npar, nc, nx = layout.N, layout.npar, layout.n_scen, layout.nx
+    S, P = sc.stage_params.shape[0], sc.n_solvers
+    nv = layout.nvar
+    i_scen = layout.idx("disc_0_scenario_constraint_0_a1")
+    params = np.repeat(np.repeat(sc.stage_params[:, None, None, :], P, 1), N, 2).reshape(S * P, N, npar)
+    warm = np.zeros((S * P, N + 1, nv))
+    xinit = np.repeat(sc.state, P, 0).copy()
+    for s_ in range(S):
+        w = sc.main_warm[s_] if sc.main_warm is not None else braking_warm(sc.state[s_], N, layout.dt, nv,
+                                                                             deceleration)
+        for p_ in range(P):
+            b = s_ * P + p_
+            warm[b] = w
+            rows = np.zeros((N, nc, 3))
             rows[0] = (0.0, 0.0, DUMMY_B)
             for k in range(1, N):
-                rows[k] = reduce_samples(samples[:, :, k].reshape(-1, 2), w[k, 2:4], nc,
-                                         ROBOT_RADIUS + OBSTACLE_RADIUS)
-            warm[b] = w
-            xinit[b] = x0
-    return ScenarioBatch(params=params, warm=warm, xinit=xinit, n_scenes=B, n_solvers=P)
+                rows[k] = reduce_samples(sc.samples[b, k], w[k, 2:4], nc, radius)
+            params[b, :, i_scen:i_scen + 3 * nc] = rows.reshape(N, 3 * nc)
+    return ScenarioBatch(params=params, warm=warm, xinit=xinit, n_scenes=S, n_solvers=P, scenes=sc)
+
+
+def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
+                     n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioBatch:
+    sc = make_shmpc_scenes(layout, n_scenes, n_solvers, n_obs, n_samples, seed, first_scene)
+    return prepare_scenario_host(layout, sc)
 
 
 def select_lowest_cost(pobj: np.ndarray, exit_code: np.ndarray, n_solvers: int) -> np.ndarray:

@@ -1,0 +1,90 @@
+"""GPU SH-MPC producers (mpcg_prepare_scenario, mpcg_select_lowest_cost_device)
+against their host restatement (scenario.py): bit-exact, including ties
+between samples, fewer samples than rows and a given main warm start."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _t(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _gpu_prepare(lay, sc, dev, radius, decel):
+    from oscar_mpc_planner_mr_modification_amd import native
+    pr = native.problem_from_layout(lay)
+    out = native.prepare_scenario_device(pr, sc.n_solvers, _t(sc.stage_params, dev), _t(sc.state, dev),
+                                         _t(sc.samples, dev), radius, decel,
+                                         main_warm=None if sc.main_warm is None else _t(sc.main_warm, dev))
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("cfg", ["C5", "small"])
+def test_scenario_producer_bit_exact(dev, cfg):
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout, safe_horizon_layout
+    from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_scenes, prepare_scenario_host
+    lay = config_layout("C5") if cfg == "C5" else safe_horizon_layout(N=10, n_constraints=4)
+    sc = make_shmpc_scenes(lay, 6, n_obs=12 if cfg == "C5" else 3, n_samples=100 if cfg == "C5" else 7, seed=77)
+    # exact ties: duplicate one solver's stage-3 samples
+    sc.samples[1, 3, 5:10] = sc.samples[1, 3, 0:5]
+    ref = prepare_scenario_host(lay, sc, 0.65, 3.0)
+    got = _gpu_prepare(lay, sc, dev, 0.65, 3.0)
+    for k in ("params", "warm", "xinit"):
+        assert np.array_equal(got[k], getattr(ref, k)), (k, np.abs(got[k] - getattr(ref, k)).max())
+
+
+def test_scenario_producer_few_samples_and_main_warm(dev):
+    from oscar_mpc_planner_mr_modification_amd.layouts import safe_horizon_layout
+    from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_scenes, prepare_scenario_host
+    lay = safe_horizon_layout(N=10, n_constraints=4)
+    sc = make_shmpc_scenes(lay, 3, n_obs=1, n_samples=2, seed=5)   # M = 2 < 4 rows
+    rng = np.random.default_rng(0)
+    sc.main_warm = rng.normal(size=(3, lay.N + 1, lay.nvar))
+    ref = prepare_scenario_host(lay, sc, 0.65, 3.0)
+    got = _gpu_prepare(lay, sc, dev, 0.65, 3.0)
+    for k in ("params", "warm", "xinit"):
+        assert np.array_equal(got[k], getattr(ref, k)), k
+
+
+def test_select_lowest_cost_device(dev):
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.scenario import select_lowest_cost
+    rng = np.random.default_rng(1)
+    S, P = 300, 4
+    pobj = rng.choice([1.0, 2.0, 3.0, 5e8, 2e9], size=S * P)
+    ex = rng.choice([0, 1, 4], size=S * P).astype(np.int32)
+    best = native.select_lowest_cost_device(S, P, _t(pobj, dev), _t(ex, dev)).cpu().numpy()
+    assert np.array_equal(best, select_lowest_cost(pobj, ex, P))
+
+
+def test_shmpc_pipeline_matches_oracle(dev, oracle_mod):
+    """producer -> solve -> pick on the GPU against host producer -> oracle -> pick."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.scenario import (make_shmpc_scenes, prepare_scenario_host,
+                                                                select_lowest_cost)
+    lay = config_layout("C5")
+    sc = make_shmpc_scenes(lay, 8, seed=123)
+    hb = prepare_scenario_host(lay, sc)
+    ref = oracle_mod.Oracle(lay).solve_batch(hb.params, hb.warm, hb.xinit)
+    pr = native.problem_from_layout(lay)
+    inp = native.prepare_scenario_device(pr, sc.n_solvers, _t(sc.stage_params, dev), _t(sc.state, dev),
+                                         _t(sc.samples, dev), 0.65, 3.0)
+    out = native.solve_batch_device(pr, inp["params"], inp["warm"], inp["xinit"])
+    best = native.select_lowest_cost_device(8, sc.n_solvers, out["pobj"], out["exit"])
+    torch.cuda.synchronize()
+    ex = out["exit"].cpu().numpy()
+    assert np.array_equal(ex, ref["status"])
+    ok = ex == 1
+    assert np.abs(out["xtraj"].cpu().numpy()[ok] - ref["xtraj"][ok]).max() <= 1e-4
+    assert np.array_equal(best.cpu().numpy(), select_lowest_cost(ref["pobj"], ref["status"], sc.n_solvers))
