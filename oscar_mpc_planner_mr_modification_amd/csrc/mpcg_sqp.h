@@ -366,16 +366,21 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 R.l[s] = pr.qp_mu0 / t0;
                 R.pr[s] = 0.0;
             };
+            // every slot is (re)written, inactive ones with placeholders that are never
+            // read: the row state is then dead between two QPs and the linearisation
+            // does not have to keep it in registers
 #pragma unroll
             for (int j = 0; j < BVS; ++j) {
-                if (!LR.box_on(j)) continue;
-                const double zv = S.z[k][LR.var(j)];
-                cold(2 * j, zv - LR.lo[j]);
-                cold(2 * j + 1, LR.hi[j] - zv);
+                const bool on = LR.box_on(j);
+                const double zv = S.z[ks][on ? LR.var(j) : 0];
+                cold(2 * j, on ? zv - LR.lo[j] : 1.0);
+                cold(2 * j + 1, on ? LR.hi[j] - zv : 1.0);
             }
 #pragma unroll
-            for (int r = 0; r < HS; ++r)
-                if (LR.h_on(r)) cold(HB + r, S.hd[k][LR.hrow(r)]);
+            for (int r = 0; r < HS; ++r) {
+                const bool on = LR.h_on(r);
+                cold(HB + r, on ? S.hd[kc][on ? LR.hrow(r) : 0] : 1.0);
+            }
         }
         if (stage_lane) {
 #pragma unroll
@@ -418,12 +423,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         rb = R.l[2 * j + 1] - R.l[2 * j];
                         row_res(2 * j, -dzv, zv - LR.lo[j]);
                         row_res(2 * j + 1, dzv, LR.hi[j] - zv);
+                    } else {
+                        R.rin[2 * j] = R.rin[2 * j + 1] = 0.0;
+                        R.it[2 * j] = R.it[2 * j + 1] = 1.0;
                     }
                     if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = rb;
                 }
 #pragma unroll
                 for (int r = 0; r < HS; ++r) {
-                    if (!LR.h_on(r)) continue;
+                    if (!LR.h_on(r)) {
+                        R.rin[HB + r] = 0.0;
+                        R.it[HB + r] = 1.0;
+                        continue;
+                    }
                     const int hh = LR.hrow(r);
                     const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2], l = R.l[HB + r];
                     rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;

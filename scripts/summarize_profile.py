@@ -27,7 +27,8 @@ def counters(path):
     meta = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        key = next((k for k in ("sqp_kernel", "select_best_kernel", "prepare_kernel") if k in name), None)
+        key = next((k for k in ("sqp_kernel", "select_best_kernel", "select_lowest_cost_kernel",
+                                "scenario_prepare_kernel", "prepare_kernel") if k in name), None)
         if key is None:
             continue
         agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -96,11 +97,13 @@ def main():
     json.dump(res, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
     sq = res["kernels"].get("sqp_kernel", {})
     if "hbm_bytes_per_launch" in sq:
-        json.dump({"tag": tag, "config": args.config, "batch": args.batch,
-                   "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
-                   "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"],
-                   "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch")},
-                  open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
+        tr = {"tag": tag, "config": args.config, "batch": args.batch,
+              "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
+              "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"],
+              "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch")}
+        json.dump(tr, open(os.path.join(out, f"traffic_{args.config}.json"), "w"), indent=1)
+        if args.config == "C2":
+            json.dump(tr, open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 

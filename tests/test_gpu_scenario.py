@@ -1,6 +1,12 @@
 """GPU SH-MPC producers (mpcg_prepare_scenario, mpcg_select_lowest_cost_device)
-against their host restatement (scenario.py): bit-exact, including ties
-between samples, fewer samples than rows and a given main warm start."""
+against their host restatement (scenario.py), including ties between samples,
+fewer samples than rows and a given main warm start.
+
+The braking plan's cos/sin (device ocml vs host libm) may differ in the last
+ulp, and the halfspaces are taken at those positions: warm starts and rows
+agree to 1e-12 (a different sample choice would differ by O(1)); with a given
+main warm start (no transcendental on the path) everything is bit-exact, as is
+the pick."""
 import numpy as np
 import pytest
 
@@ -36,6 +42,13 @@ def test_scenario_producer_bit_exact(dev, cfg):
     sc = make_shmpc_scenes(lay, 6, n_obs=12 if cfg == "C5" else 3, n_samples=100 if cfg == "C5" else 7, seed=77)
     # exact ties: duplicate one solver's stage-3 samples
     sc.samples[1, 3, 5:10] = sc.samples[1, 3, 0:5]
+    ref = prepare_scenario_host(lay, sc, 0.65, 3.0)
+    got = _gpu_prepare(lay, sc, dev, 0.65, 3.0)
+    assert np.array_equal(got["xinit"], ref.xinit)
+    for k in ("params", "warm"):
+        np.testing.assert_allclose(got[k], getattr(ref, k), rtol=0, atol=1e-12, err_msg=k)
+    # bit-exact once the warm start is given (no transcendental on the path)
+    sc.main_warm = ref.warm[::sc.n_solvers].copy()
     ref = prepare_scenario_host(lay, sc, 0.65, 3.0)
     got = _gpu_prepare(lay, sc, dev, 0.65, 3.0)
     for k in ("params", "warm", "xinit"):
