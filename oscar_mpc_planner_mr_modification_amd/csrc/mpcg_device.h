@@ -296,8 +296,10 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + 
 // so decoupled sub-blocks (e.g. {a,w,psi,v} vs {x,y,s} with a zero disc
 // offset) cost only their own rotations.
 // ---------------------------------------------------------------------------
+// dia_extra: squared diagonal of a decoupled block handled outside (it enters
+// the convergence test exactly as in the full-size sweep)
 template <int NZ>
-__device__ inline void mirror(double A[NZ][NZ], double eps) {
+__device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0.0) {
     // Cyclic Jacobi on the symmetric part, one-sided rotation updates on the
     // upper triangle (a_pp -= t a_pq, a_qq += t a_pq, off-diagonal pairs with
     // tau = s / (1 + c)); V accumulates the eigenvectors.  Then
@@ -315,6 +317,7 @@ __device__ inline void mirror(double A[NZ][NZ], double eps) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i) {
             dia += A[i][i] * A[i][i];
+            if (i == NZ - 1) dia += dia_extra;
 #pragma unroll
             for (int j = i + 1; j < NZ; ++j) off += A[i][j] * A[i][j];
         }

@@ -62,6 +62,9 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
+    // 1/t of every row kept in registers when the row state is small; long
+    // horizons (PARTS = 2, more rows per lane) recompute it to stay out of scratch
+    static constexpr bool STORE_IT = SLOTS <= 12;
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
@@ -150,7 +153,14 @@ __device__ __forceinline__ double dh_at(const double* dh, int i, int j) {
 // Register state of the inequality rows a lane owns (slot s).
 template <class C>
 struct Rows {
-    double t[C::SLOTS], l[C::SLOTS], it[C::SLOTS], rin[C::SLOTS], pr[C::SLOTS];
+    double t[C::SLOTS], l[C::SLOTS], it_[C::STORE_IT ? C::SLOTS : 1], rin[C::SLOTS], pr[C::SLOTS];
+    __device__ __forceinline__ double it(int s) const {
+        if constexpr (C::STORE_IT) return it_[s];
+        else return frcp(t[s]);
+    }
+    __device__ __forceinline__ void set_it(int s, double v) {
+        if constexpr (C::STORE_IT) it_[s] = v;
+    }
     double nlam[C::HS];  // NLP multiplier of the h row (Hessian weight of the next linearisation)
 };
 
@@ -336,7 +346,26 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
                 H[4][4] += hb6[5];
                 STAMP_LAP(13);
-                mirror<NZ>(H, pr.reg_eps);
+                if constexpr (NZ == 8) {
+                    // the slack row/column of the slack model is exactly zero off the
+                    // diagonal (quadratic slack cost, linear in every h row, no dynamics
+                    // coupling): MIRROR of the 8x8 block = MIRROR of the leading 7x7 block
+                    // plus the mirrored slack diagonal, with the same sweep count
+                    double H7[NZ - 1][NZ - 1];
+#pragma unroll
+                    for (int i = 0; i < NZ - 1; ++i)
+#pragma unroll
+                        for (int j = 0; j < NZ - 1; ++j) H7[i][j] = H[i][j];
+                    const double hs = H[NZ - 1][NZ - 1];
+                    mirror<NZ - 1>(H7, pr.reg_eps, hs * hs);
+#pragma unroll
+                    for (int i = 0; i < NZ - 1; ++i)
+#pragma unroll
+                        for (int j = 0; j < NZ - 1; ++j) H[i][j] = H7[i][j];
+                    H[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
+                } else {
+                    mirror<NZ>(H, pr.reg_eps);
+                }
                 STAMP_LAP(14);
 #pragma unroll
                 for (int i = 0; i < NZ; ++i)
@@ -410,7 +439,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     const double l = R.l[s], t = R.t[s];
                     const double rin = ddot + t - gap;
                     R.rin[s] = rin;
-                    R.it[s] = frcp(t);
+                    R.set_it(s, frcp(t));
                     ri = fmax(ri, fabs(rin));
                     comp += l * t;
                 };
@@ -425,7 +454,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         row_res(2 * j + 1, dzv, LR.hi[j] - zv);
                     } else {
                         R.rin[2 * j] = R.rin[2 * j + 1] = 0.0;
-                        R.it[2 * j] = R.it[2 * j + 1] = 1.0;
+                        R.set_it(2 * j, 1.0);
+                        R.set_it(2 * j + 1, 1.0);
                     }
                     if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = rb;
                 }
@@ -433,7 +463,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int r = 0; r < HS; ++r) {
                     if (!LR.h_on(r)) {
                         R.rin[HB + r] = 0.0;
-                        R.it[HB + r] = 1.0;
+                        R.set_it(HB + r, 1.0);
                         continue;
                     }
                     const int hh = LR.hrow(r);
@@ -520,7 +550,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     for (int i = 0; i < NBT; ++i) dbh[i] = 0.0;
                     // coef = l + (l rin - rc) / t, wgt = l / t of slot s
                     auto bar = [&](int s, double& coef, double& wgt) {
-                        const double l = R.l[s], t = R.t[s], itt = R.it[s];
+                        const double l = R.l[s], t = R.t[s], itt = R.it(s);
                         const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
                         coef = l + (l * R.rin[s] - rc) * itt;
                         wgt = l * itt;
@@ -819,7 +849,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const double l = R.l[s], t = R.t[s];
                         const double rc = (ph == 0) ? l * t : l * t + R.pr[s] - smu;
                         dt = -R.rin[s] - ddot(s);
-                        dl = -(rc + l * dt) * R.it[s];
+                        dl = -(rc + l * dt) * R.it(s);
                     };
                     // step to the boundary: min over rows of -t/dt and -l/dl = 1 / max(-dt/t, -dl/l)
                     double rmax = 0.0;
@@ -828,7 +858,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         if (!active(s)) continue;
                         double dt, dl;
                         row_step(s, dt, dl);
-                        rmax = fmax(rmax, -dt * R.it[s]);
+                        rmax = fmax(rmax, -dt * R.it(s));
                         if (dl < 0.0) rmax = fmax(rmax, -dl * frcp(R.l[s]));
                     }
                     rmax = wave_max(rmax);
