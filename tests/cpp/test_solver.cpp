@@ -76,7 +76,8 @@ static void test_plumbing() {
     CHECK(solver.dt > 0.);
     CHECK(solver.N == SOLVER_N);
     CHECK(solver._num_iterations == 10);
-    CHECK(solver.problem().n_lin + solver.problem().n_ell == SOLVER_NH);
+    CHECK(solver.problem().n_lin + solver.problem().n_ell + solver.problem().n_scen == SOLVER_NH);
+    CHECK(solver.problem().nx == SOLVER_NX);
     CHECK((int)solver.multipliers().size() == SOLVER_N * (SOLVER_NX + SOLVER_NH));
 
     for (int k = 0; k < solver.N; k++) solver.setParameter(k, "reference_velocity", 1.);
@@ -92,10 +93,21 @@ static void test_plumbing() {
     CHECK(solver.getParameter(2, "acceleration") == 0.34);
     setSolverParameterSplineXA(4, solver._params, 7.0, 2);
     CHECK(solver.getParameter(4, "spline_x2_a") == 7.0);
+#if SOLVER_N_ELL > 1
     setSolverParameterEllipsoidObstPsi(5, solver._params, 0.5, 1);
     CHECK(solver.getParameter(5, "ellipsoid_obst_1_psi") == 0.5);
+#endif
+#if SOLVER_N_LIN > 3
     setSolverParameterLinConstraintB(6, solver._params, -1.25, 3);
     CHECK(solver.getParameter(6, "lin_constraint_3_b") == -1.25);
+#endif
+#if SOLVER_N_SCEN > 3
+    // scenario_constraints.py:41-50: one bundle per scalar
+    setSolverParameterDisc0ScenarioConstraint3B(6, solver._params, -1.25);
+    CHECK(solver.getParameter(6, "disc_0_scenario_constraint_3_b") == -1.25);
+    setSolverParameterSlack(1, solver._params, 10000.);
+    CHECK(solver.getParameter(1, "slack") == 10000.);
+#endif
 
     solver.setXinit("x", 5.4);
     solver.setXinit("y", 1.4);
@@ -189,8 +201,8 @@ static Batch read_batch(const char* path) {
     b.npar = h[2];
     b.iters = h[3];
     b.params.resize((size_t)b.B * b.N * b.npar);
-    b.warm.resize((size_t)b.B * (b.N + 1) * 7);
-    b.xinit.resize((size_t)b.B * 5);
+    b.warm.resize((size_t)b.B * (b.N + 1) * (SOLVER_NU + SOLVER_NX));
+    b.xinit.resize((size_t)b.B * SOLVER_NX);
     f.read(reinterpret_cast<char*>(b.params.data()), b.params.size() * 8);
     f.read(reinterpret_cast<char*>(b.warm.data()), b.warm.size() * 8);
     f.read(reinterpret_cast<char*>(b.xinit.data()), b.xinit.size() * 8);
@@ -200,8 +212,9 @@ static Batch read_batch(const char* path) {
 
 static void load(Solver& s, const Batch& b, int i) {
     std::memcpy(s._params.all_parameters, &b.params[(size_t)i * b.N * b.npar], sizeof(double) * b.N * b.npar);
-    std::memcpy(s._params.x0, &b.warm[(size_t)i * (b.N + 1) * 7], sizeof(double) * (b.N + 1) * 7);
-    std::memcpy(s._params.xinit, &b.xinit[(size_t)i * 5], sizeof(double) * 5);
+    const size_t nv = SOLVER_NU + SOLVER_NX;
+    std::memcpy(s._params.x0, &b.warm[(size_t)i * (b.N + 1) * nv], sizeof(double) * (b.N + 1) * nv);
+    std::memcpy(s._params.xinit, &b.xinit[(size_t)i * SOLVER_NX], sizeof(double) * SOLVER_NX);
     s.loadWarmstart();
 }
 

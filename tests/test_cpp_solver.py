@@ -34,6 +34,12 @@ def cpp_build():
     return _build.build_cpp("C2")
 
 
+@pytest.fixture(scope="module")
+def cpp_build_c5():
+    from oscar_mpc_planner_mr_modification_amd import _build
+    return _build.build_cpp("C5")
+
+
 def _env(d):
     env = dict(os.environ)
     env["MPCG_SOLVER_DIR"] = d
@@ -73,6 +79,14 @@ def test_cpp_solver_plumbing(cpp_build):
     assert "OK plumbing" in r.stdout
 
 
+def test_cpp_solver_plumbing_slack_model(cpp_build_c5):
+    """The same drop-in compiled for the SH-MPC solver (nx 6, scenario rows)."""
+    r = subprocess.run([cpp_build_c5["test"], "plumbing"], env=_env(cpp_build_c5["dir"]), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK plumbing" in r.stdout
+
+
 def test_cpp_solver_rejects_mismatched_settings(cpp_build, tmp_path):
     """A solver directory whose dimensions differ from the compiled ones is
     refused at construction (the reference exits when its capsule cannot be
@@ -85,11 +99,15 @@ def test_cpp_solver_rejects_mismatched_settings(cpp_build, tmp_path):
 
 
 @pytest.mark.gpu
-def test_cpp_solver_on_gpu_matches_oracle(cpp_build, oracle_mod, tmp_path):
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_cpp_solver_on_gpu_matches_oracle(cpp_build, cpp_build_c5, oracle_mod, tmp_path, cfg):
+    from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_batch
     from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
-    lay = config_layout("C2")
-    b = make_batch(lay, 3, 8, seed=8080)
-    B, N = b.params.shape[0], lay.N
+    lay = config_layout(cfg)
+    b = make_batch(lay, 3, 8, seed=8080) if cfg == "C2" else make_shmpc_batch(lay, 6, seed=8080)
+    if cfg == "C5":
+        cpp_build = cpp_build_c5
+    B, N, nx = b.params.shape[0], lay.N, lay.nx
     fin = tmp_path / "in.bin"
     with open(fin, "wb") as fh:
         np.array([B, N, lay.npar, 10], np.int32).tofile(fh)
@@ -99,12 +117,12 @@ def test_cpp_solver_on_gpu_matches_oracle(cpp_build, oracle_mod, tmp_path):
     r = subprocess.run([cpp_build["test"], "solve", str(fin), str(fout)], env=_env(cpp_build["dir"]),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    rec = (N + 1) * 5 + N * 2 + 3
+    rec = (N + 1) * nx + N * 2 + 3
     raw = np.fromfile(fout, np.float64).reshape(-1, B, rec)
     assert raw.shape[0] == 5  # solve x2, batch x2, one-iteration
 
     def split(a):
-        return dict(xtraj=a[:, :(N + 1) * 5].reshape(B, N + 1, 5), utraj=a[:, (N + 1) * 5:-3].reshape(B, N, 2),
+        return dict(xtraj=a[:, :(N + 1) * nx].reshape(B, N + 1, nx), utraj=a[:, (N + 1) * nx:-3].reshape(B, N, 2),
                     pobj=a[:, -3], exit=a[:, -2].astype(np.int32))
 
     step1, step2, batch1, batch2, oneit = (split(raw[i]) for i in range(5))
