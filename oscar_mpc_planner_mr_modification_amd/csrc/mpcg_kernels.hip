@@ -242,11 +242,11 @@ int mpcg_solve(const mpcg_problem* pr, int batch, const mpcg_io* io, void* strea
     mpcg::Fn fn;
     int rc = mpcg::check_problem(pr, batch, &fn);
     if (rc) return rc;
+    if (batch == 0) return 0;  // nothing to do: buffers may be NULL
     if (!io || !io->params || !io->warm || !io->xinit || !io->xtraj || !io->utraj || !io->pobj || !io->exit_code) {
         mpcg::g_err = "missing buffer";
         return -1;
     }
-    if (batch == 0) return 0;
     return fn(*pr, batch, *io, (hipStream_t)stream);
 }
 
@@ -308,11 +308,11 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
         mpcg::g_err = "mpcg_context_solve: invalid arguments or batch > max_batch";
         return -1;
     }
+    if (batch == 0) return 0;  // nothing to do: buffers may be NULL
     if (!io->params || !io->warm || !io->xinit || !io->xtraj || !io->utraj || !io->pobj || !io->exit_code) {
         mpcg::g_err = "missing buffer";
         return -1;
     }
-    if (batch == 0) return 0;
     const mpcg_problem& pr = c->pr;
     const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr);
     const size_t nx = pr.nx;

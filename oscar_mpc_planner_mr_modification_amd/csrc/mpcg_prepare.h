@@ -330,22 +330,47 @@ namespace mpcg {
 // One workgroup of 4 wavefronts per (scene, parallel solver):
 //   warm start   main warm start or the braking plan (acados_solver_interface.cpp:303-342)
 //   halfspaces   wave w reduces stages k = 1 + w, 5 + w, ...: each lane holds the distances
-//                of samples lane, lane + 64, ... to the warm-start position p_k in registers,
-//                then n_scen wave arg-min rounds (distance, then sample index: the stable
-//                order of the host's argsort) pick the closest samples; row
+//                of samples lane, lane + 64, ... to the warm-start position p_k in registers
+//                and a sorted list of its 4 closest; n_scen DPP wave arg-min rounds over the
+//                list heads (distance, then sample index: the stable order of the host's
+//                argsort) pick the closest samples, the winning lane pops its head and a
+//                lane whose list runs dry rebuilds it from the samples after its last pick; row
 //                n = (q - p_k) / max(|q - p_k|, 1e-9), b = n . q - radius
 //   stage 0      inactive rows (0, 0, 100)
 // then the N x npar parameter block is streamed out with coalesced stores.
 // Memory bound: every sample is read once (N-1 stages x M x 16 B per solve).
 // ---------------------------------------------------------------------------
 constexpr int SCEN_MAX_N = 32, SCEN_MAX_ROWS = 32, SCEN_PER_LANE = 32;  // M <= 64 * 32
+constexpr int SCEN_TOPK = 4;  // per-lane candidate list of the arg-min rounds
 constexpr double SCEN_DUMMY_B = 100.0;
+
+__device__ __forceinline__ double readlane_dbl(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// one DPP step of a wave arg-min over (distance, index): lanes outside the
+// row mask compare with themselves
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_argmin_step(double& d, int& i) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(d), __double2loint(d), CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(d), __double2hiint(d), CTRL, ROWS, 0xf, false);
+    const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWS, 0xf, false);
+    const double od = __hiloint2double(hi, lo);
+    if (od < d || (od == d && oi < i)) {
+        d = od;
+        i = oi;
+    }
+}
 
 struct ScenLds {
     double warm[SCEN_MAX_N + 1][MPCG_NU + MPCG_MAX_NX];
     double rows[SCEN_MAX_N][SCEN_MAX_ROWS][3];
 };
 
+// PL: samples per lane held in registers (M <= 64 PL); instances 8 / 20 / 32
+template <int PL>
 __global__ __launch_bounds__(256) void scenario_prepare_kernel(mpcg_problem pr, int n_scenes, int P,
                                                                mpcg_scenario_io in, double* __restrict__ params,
                                                                double* __restrict__ warm,
@@ -383,34 +408,71 @@ __global__ __launch_bounds__(256) void scenario_prepare_kernel(mpcg_problem pr, 
 
     // ---- sample -> halfspace reduction, one stage per wave at a time
     const double INF = __longlong_as_double(0x7ff0000000000000LL);
+    constexpr int BIG = 0x7fffffff;
     for (int k = 1 + wave; k < N; k += 4) {
         const double* q = in.samples + ((size_t)sol * N + k) * (size_t)M * 2;
         const double rx = L.warm[k][2], ry = L.warm[k][3];
-        double dist[SCEN_PER_LANE];
+        double dist[PL];
+        int left = 0;  // samples of this lane not picked yet
 #pragma unroll
-        for (int j = 0; j < SCEN_PER_LANE; ++j) {
+        for (int j = 0; j < PL; ++j) {
             const int i = lane + 64 * j;
             double d = INF;
-            if (i < M) d = norm2_rn(__dsub_rn(q[2 * i], rx), __dsub_rn(q[2 * i + 1], ry));
+            if (i < M) {
+                d = norm2_rn(__dsub_rn(q[2 * i], rx), __dsub_rn(q[2 * i + 1], ry));
+                ++left;
+            }
             dist[j] = d;
         }
-        for (int r = 0; r < NS; ++r) {
-            double bd = INF;
-            int bi = 0x7fffffff;
+        // each lane keeps its SCEN_TOPK closest samples sorted by (distance, index); the
+        // list is rebuilt from the samples after the last pick when it runs dry
+        double td[SCEN_TOPK];
+        int ti[SCEN_TOPK];
+        double lastd = -1.0;
+        int lasti = -1;
+        auto rebuild = [&]() {
 #pragma unroll
-            for (int j = 0; j < SCEN_PER_LANE; ++j)
-                if (dist[j] < bd) { bd = dist[j]; bi = lane + 64 * j; }
+            for (int t = 0; t < SCEN_TOPK; ++t) { td[t] = INF; ti[t] = BIG; }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double od = __shfl_xor(bd, o);
-                const int oi = __shfl_xor(bi, o);
-                if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+            for (int j = 0; j < PL; ++j) {
+                double x = dist[j];
+                int xi = lane + 64 * j;
+                if (!(x > lastd || (x == lastd && xi > lasti))) continue;
+#pragma unroll
+                for (int t = 0; t < SCEN_TOPK; ++t)
+                    if (x < td[t]) {  // strict: equal distances keep the lower index first
+                        const double y = td[t];
+                        const int yi = ti[t];
+                        td[t] = x; ti[t] = xi;
+                        x = y; xi = yi;
+                    }
             }
+        };
+        rebuild();
+        for (int r = 0; r < NS; ++r) {
+            // wave arg-min of the list heads over (distance, index) through DPP
+            double bd = td[0];
+            int bi = ti[0];
+            dpp_argmin_step<0xB1, 0xf>(bd, bi);   // quad_perm [1,0,3,2]
+            dpp_argmin_step<0x4E, 0xf>(bd, bi);   // quad_perm [2,3,0,1]
+            dpp_argmin_step<0x124, 0xf>(bd, bi);  // row_ror:4
+            dpp_argmin_step<0x128, 0xf>(bd, bi);  // row_ror:8
+            dpp_argmin_step<0x142, 0xa>(bd, bi);  // row_bcast:15
+            dpp_argmin_step<0x143, 0xc>(bd, bi);  // row_bcast:31
+            bd = readlane_dbl(bd, 63);
+            bi = __builtin_amdgcn_readlane(bi, 63);
             const bool found = bi < M;
             if (found && lane == (bi & 63)) {
+                lastd = td[0];
+                lasti = ti[0];
+                --left;
 #pragma unroll
-                for (int j = 0; j < SCEN_PER_LANE; ++j)
-                    if (j == (bi >> 6)) dist[j] = INF;
+                for (int t = 0; t + 1 < SCEN_TOPK; ++t) { td[t] = td[t + 1]; ti[t] = ti[t + 1]; }
+                td[SCEN_TOPK - 1] = INF;
+                ti[SCEN_TOPK - 1] = BIG;
+            }
+            if (__any(left > 0 && ti[0] == BIG)) {
+                if (left > 0 && ti[0] == BIG) rebuild();
             }
             if (lane == 0) {
                 double a1 = 0.0, a2 = 0.0, b = 0.0;

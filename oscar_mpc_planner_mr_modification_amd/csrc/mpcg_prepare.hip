@@ -82,8 +82,11 @@ int mpcg_prepare_scenario(const mpcg_problem* pr, int n_scenes, int n_solvers, c
         return -2;
     }
     if (n_scenes == 0) return 0;
-    hipLaunchKernelGGL(mpcg::scenario_prepare_kernel, dim3(n_scenes * n_solvers), dim3(256), 0, (hipStream_t)stream,
-                       *pr, n_scenes, n_solvers, *in, params, warm, xinit);
+    const int M = in->n_samples;
+    auto kern = M <= 64 * 8 ? mpcg::scenario_prepare_kernel<8>
+                            : (M <= 64 * 20 ? mpcg::scenario_prepare_kernel<20> : mpcg::scenario_prepare_kernel<32>);
+    hipLaunchKernelGGL(kern, dim3(n_scenes * n_solvers), dim3(256), 0, (hipStream_t)stream, *pr, n_scenes, n_solvers,
+                       *in, params, warm, xinit);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         mpcg::g_err = std::string("scenario prepare launch: ") + hipGetErrorString(e);
