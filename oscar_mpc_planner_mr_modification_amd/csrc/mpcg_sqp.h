@@ -66,6 +66,12 @@ struct Cfg {
     // horizons (PARTS = 2, more rows per lane) recompute it to stay out of scratch
     static constexpr bool STORE_IT = SLOTS <= 12;
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
+    // Linear rows (topology and scenario halfspaces) read their coefficients from the
+    // parameter block instead of LDS, and their gaps are recomputed from the iterate:
+    // only the ellipsoid rows keep gradients / gaps in LDS.  Used where it lowers the
+    // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
+    static constexpr bool LIN_PARAMS = NS > 0;
+    static constexpr int NHS = LIN_PARAMS ? (NE > 0 ? NE : 1) : NH;  // rows with LDS storage
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
     __host__ __device__ static constexpr int blk(int v) {
@@ -97,8 +103,9 @@ struct Lds {
     double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
     double Y[N][NU][NX];      // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
-    double Dg[N][C::NH][3];   // signed h-row gradients on (x, y, psi); the slack one is C::slack_coef
-    double hd[N][C::NH];      // h-row bound gaps (uh - h or h - lh)
+    double Dg[N][C::NHS][3];  // signed h-row gradients on (x, y, psi); the slack one is C::slack_coef
+    double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
+    double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
     double Msc[C::NTRI];      // factorisation scratch
     double xinit[NX];
     int flag;
@@ -185,18 +192,22 @@ struct LaneRows {
 template <class C>
 __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[C::NZ],
                                        const LaneRows<C>& LR, const double* nlam, double hb6[6], double (*Dg)[3],
-                                       double* hd) {
+                                       double* hd, double* disc) {
     const double x = z[2], y = z[3], psi = z[4];
     const double rdisc = C::NE > 0 ? pk[pr.i_disc_r] : 0.0, off = pk[pr.i_disc_off];
     double sp, cp;
     sincos(psi, &sp, &cp);
     const double dxp = -off * sp, dyp = off * cp, dxpp = -off * cp, dypp = -off * sp;
+    if constexpr (C::LIN_PARAMS) {
+        if (LR.part == 0) { disc[0] = off * cp; disc[1] = off * sp; disc[2] = dxp; disc[3] = dyp; }
+    }
 #pragma unroll
     for (int r = 0; r < C::HS; ++r) {
         if (!LR.h_on(r)) continue;
         const int hh = LR.hrow(r);
         if (hh < C::NL) {
             // topology halfspace a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370)
+            if constexpr (C::LIN_PARAMS) continue;  // read from the parameters where used
             const double* c = pk + pr.i_lin0 + 3 * hh;
             hd[hh] = 0.0 - (c[0] * x + c[1] * y - c[2]);
             Dg[hh][0] = c[0];
@@ -206,11 +217,13 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             // scenario halfspace a1 xd + a2 yd - (b + slack) <= 0 at the disc
             // position (scenario_constraints.py:64-94)
             const double* c = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
-            const double sl = C::NX > 5 ? z[NU + 5] : 0.0;
-            hd[hh] = 0.0 - (c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl));
-            Dg[hh][0] = c[0];
-            Dg[hh][1] = c[1];
-            Dg[hh][2] = c[0] * dxp + c[1] * dyp;
+            if constexpr (!C::LIN_PARAMS) {
+                const double sl = C::NX > 5 ? z[NU + 5] : 0.0;
+                hd[hh] = 0.0 - (c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl));
+                Dg[hh][0] = c[0];
+                Dg[hh][1] = c[1];
+                Dg[hh][2] = c[0] * dxp + c[1] * dyp;
+            }
             const double wgt = nlam[r];  // upper-bound row: Hessian weight +lambda
             hb6[5] += wgt * (c[0] * dxpp + c[1] * dypp);
         } else {
@@ -227,10 +240,11 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             const double M11 = so * so * D0 + co * co * D1;
             const double ddx = x + off * cp - o[0], ddy = y + off * sp - o[1];
             const double Mdx = M00 * ddx + M01 * ddy, Mdy = M01 * ddx + M11 * ddy;
-            hd[hh] = (ddx * Mdx + ddy * Mdy) - 1.0;
-            Dg[hh][0] = -2.0 * Mdx;
-            Dg[hh][1] = -2.0 * Mdy;
-            Dg[hh][2] = -2.0 * (Mdx * dxp + Mdy * dyp);
+            const int he = C::LIN_PARAMS ? hh - C::NL : hh;
+            hd[he] = (ddx * Mdx + ddy * Mdy) - 1.0;
+            Dg[he][0] = -2.0 * Mdx;
+            Dg[he][1] = -2.0 * Mdy;
+            Dg[he][2] = -2.0 * (Mdx * dxp + Mdy * dyp);
             const double wgt = -nlam[r];  // lower-bound row: Hessian weight -lambda
             if (wgt != 0.0) {
                 const double hxp = 2.0 * (M00 * dxp + M01 * dyp);
@@ -282,6 +296,39 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         LR.lo[j] = lo;
         LR.hi[j] = hi;
     }
+    // gradient (x, y, psi) and gap of h row hh of this lane's stage
+    auto rowg = [&](int hh, double& a, double& b, double& c) {
+        if constexpr (C::LIN_PARAMS) {
+            if (hh < C::NL || hh >= C::NL + C::NE) {
+                const double* p = hh < C::NL ? pk + pr.i_lin0 + 3 * hh : pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
+                a = p[0];
+                b = p[1];
+                c = hh < C::NL ? 0.0 : p[0] * S.disc[k][2] + p[1] * S.disc[k][3];
+                return;
+            }
+            const int he = hh - C::NL;
+            a = S.Dg[k][he][0]; b = S.Dg[k][he][1]; c = S.Dg[k][he][2];
+        } else {
+            a = S.Dg[k][hh][0]; b = S.Dg[k][hh][1]; c = S.Dg[k][hh][2];
+        }
+    };
+    auto rowgap = [&](int hh) -> double {
+        if constexpr (C::LIN_PARAMS) {
+            const double x = S.z[k][2], y = S.z[k][3];
+            if (hh < C::NL) {
+                const double* p = pk + pr.i_lin0 + 3 * hh;
+                return 0.0 - (p[0] * x + p[1] * y - p[2]);
+            }
+            if (hh >= C::NL + C::NE) {
+                const double* p = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
+                const double sl = C::NX > 5 ? S.z[k][NU + 5] : 0.0;
+                return 0.0 - (p[0] * (x + S.disc[k][0]) + p[1] * (y + S.disc[k][1]) - (p[2] + sl));
+            }
+            return S.hd[k][hh - C::NL];
+        } else {
+            return S.hd[k][hh];
+        }
+    };
     Rows<C> R;
 #pragma unroll
     for (int r = 0; r < HS; ++r) R.nlam[r] = (lam_in && LR.h_on(r)) ? lam_in[(size_t)k * LAMS + NX + LR.hrow(r)] : 0.0;
@@ -308,7 +355,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
             double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k]);
+            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
             STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {
@@ -408,7 +455,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int r = 0; r < HS; ++r) {
                 const bool on = LR.h_on(r);
-                cold(HB + r, on ? S.hd[kc][on ? LR.hrow(r) : 0] : 1.0);
+                cold(HB + r, on ? rowgap(on ? LR.hrow(r) : 0) : 1.0);
             }
         }
         if (stage_lane) {
@@ -467,7 +514,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         continue;
                     }
                     const int hh = LR.hrow(r);
-                    const double a = S.Dg[k][hh][0], bq = S.Dg[k][hh][1], c = S.Dg[k][hh][2], l = R.l[HB + r];
+                    double a, bq, c;
+                    rowg(hh, a, bq, c);
+                    const double l = R.l[HB + r];
                     rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;
                     double dd = a * dzk[2] + bq * dzk[3] + c * dzk[4];
                     if constexpr (NB == 4) {
@@ -475,7 +524,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         rh[3] += sc * l;
                         dd += sc * dzk[ZS];
                     }
-                    row_res(HB + r, dd, S.hd[k][hh]);
+                    row_res(HB + r, dd, rowgap(hh));
                 }
                 double acc[NB];
 #pragma unroll
@@ -577,7 +626,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         double coef, wgt;
                         bar(HB + r, coef, wgt);
                         double dg[NB];
-                        dg[0] = S.Dg[k][hh][0]; dg[1] = S.Dg[k][hh][1]; dg[2] = S.Dg[k][hh][2];
+                        rowg(hh, dg[0], dg[1], dg[2]);
                         if constexpr (NB == 4) dg[3] = C::slack_coef(hh);
 #pragma unroll
                         for (int i = 0; i < NB; ++i) qh[i] += dg[i] * coef;
@@ -839,7 +888,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     auto ddot = [&](int s) {
                         if (s < HB) return (s & 1) ? ddb[s >> 1] : -ddb[s >> 1];
                         const int hh = LR.hrow(s - HB);
-                        double v = S.Dg[k][hh][0] * ddk[2] + S.Dg[k][hh][1] * ddk[3] + S.Dg[k][hh][2] * ddk[4];
+                        double ga, gb, gc;
+                        rowg(hh, ga, gb, gc);
+                        double v = ga * ddk[2] + gb * ddk[3] + gc * ddk[4];
                         if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
                         return v;
                     };
