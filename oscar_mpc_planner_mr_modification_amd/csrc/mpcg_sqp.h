@@ -70,7 +70,7 @@ struct Cfg {
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
     // only the ellipsoid rows keep gradients / gaps in LDS.  Used where it lowers the
     // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
-    static constexpr bool LIN_PARAMS = NS > 0;
+    static constexpr bool LIN_PARAMS = NS > 0 || N >= 30;
     static constexpr int NHS = LIN_PARAMS ? (NE > 0 ? NE : 1) : NH;  // rows with LDS storage
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
@@ -105,7 +105,7 @@ struct Lds {
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
     double Dg[N][C::NHS][3];  // signed h-row gradients on (x, y, psi); the slack one is C::slack_coef
     double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
-    double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
+    double disc[C::LIN_PARAMS && C::NS > 0 ? N : 1][4];  // scenario rows: off cos psi, off sin psi, d/dpsi of both
     double Msc[C::NTRI];      // factorisation scratch
     double xinit[NX];
     int flag;
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 const double* p = hh < C::NL ? pk + pr.i_lin0 + 3 * hh : pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
                 a = p[0];
                 b = p[1];
-                c = hh < C::NL ? 0.0 : p[0] * S.disc[k][2] + p[1] * S.disc[k][3];
+                c = hh < C::NL ? 0.0 : p[0] * S.disc[C::NS > 0 ? k : 0][2] + p[1] * S.disc[C::NS > 0 ? k : 0][3];
                 return;
             }
             const int he = hh - C::NL;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (hh >= C::NL + C::NE) {
                 const double* p = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
                 const double sl = C::NX > 5 ? S.z[k][NU + 5] : 0.0;
-                return 0.0 - (p[0] * (x + S.disc[k][0]) + p[1] * (y + S.disc[k][1]) - (p[2] + sl));
+                return 0.0 - (p[0] * (x + S.disc[C::NS > 0 ? k : 0][0]) + p[1] * (y + S.disc[C::NS > 0 ? k : 0][1]) - (p[2] + sl));
             }
             return S.hd[k][hh - C::NL];
         } else {
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
             double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
+            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS && C::NS > 0 ? k : 0]);
             STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {
