@@ -70,7 +70,7 @@ struct Cfg {
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
     // only the ellipsoid rows keep gradients / gaps in LDS.  Used where it lowers the
     // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
-    static constexpr bool LIN_PARAMS = NS > 0 || N >= 30;
+    static constexpr bool LIN_PARAMS = NS > 0;
     static constexpr int NHS = LIN_PARAMS ? (NE > 0 ? NE : 1) : NH;  // rows with LDS storage
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
