@@ -298,34 +298,36 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + 
 // ---------------------------------------------------------------------------
 // dia_extra: squared diagonal of a decoupled block handled outside (it enters
 // the convergence test exactly as in the full-size sweep)
-template <int NZ>
+// NA: the leading NA x NA block of the NZ x NZ array is mirrored in place
+// (NA < NZ: the trailing rows / columns are decoupled and handled by the caller)
+template <int NZ, int NA = NZ>
 __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0.0) {
     // Cyclic Jacobi on the symmetric part, one-sided rotation updates on the
     // upper triangle (a_pp -= t a_pq, a_qq += t a_pq, off-diagonal pairs with
     // tau = s / (1 + c)); V accumulates the eigenvectors.  Then
     // A = V diag(f(d)) V' with f(d) = eps if |d| <= eps else |d|.
-    double V[NZ][NZ];
+    double V[NA][NA];
 #pragma unroll
-    for (int i = 0; i < NZ; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
-        for (int j = 0; j < NZ; ++j) {
+        for (int j = 0; j < NA; ++j) {
             V[i][j] = (i == j) ? 1.0 : 0.0;
             if (j > i) A[i][j] = 0.5 * (A[i][j] + A[j][i]);
         }
     for (int sweep = 0; sweep < 50; ++sweep) {
         double off = 0.0, dia = 0.0;
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) {
+        for (int i = 0; i < NA; ++i) {
             dia += A[i][i] * A[i][i];
-            if (i == NZ - 1) dia += dia_extra;
+            if (i == NA - 1) dia += dia_extra;
 #pragma unroll
-            for (int j = i + 1; j < NZ; ++j) off += A[i][j] * A[i][j];
+            for (int j = i + 1; j < NA; ++j) off += A[i][j] * A[i][j];
         }
         if (off <= 1e-32 * dia || off < 1e-300) break;
 #pragma unroll
-        for (int p = 0; p < NZ - 1; ++p)
+        for (int p = 0; p < NA - 1; ++p)
 #pragma unroll
-            for (int q = p + 1; q < NZ; ++q) {
+            for (int q = p + 1; q < NA; ++q) {
                 const double apq = A[p][q];
                 if (fabs(apq) >= 1e-300) {
                     const double theta = 0.5 * (A[q][q] - A[p][p]) * frcp(apq);
@@ -339,7 +341,7 @@ __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0
                     A[q][q] += t * apq;
                     A[p][q] = 0.0;
 #pragma unroll
-                    for (int r = 0; r < NZ; ++r) {
+                    for (int r = 0; r < NA; ++r) {
                         if (r == p || r == q) continue;
                         double& arp = r < p ? A[r][p] : A[p][r];
                         double& arq = r < q ? A[r][q] : A[q][r];
@@ -348,7 +350,7 @@ __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0
                         arq = h + sn * fma(-h, tau, g);
                     }
 #pragma unroll
-                    for (int r = 0; r < NZ; ++r) {
+                    for (int r = 0; r < NA; ++r) {
                         const double g = V[r][p], h = V[r][q];
                         V[r][p] = g - sn * fma(g, tau, h);
                         V[r][q] = h + sn * fma(-h, tau, g);
@@ -356,19 +358,19 @@ __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0
                 }
             }
     }
-    double d[NZ];
+    double d[NA];
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) {
+    for (int i = 0; i < NA; ++i) {
         double di = A[i][i];
         d[i] = (di >= -eps && di <= eps) ? eps : fabs(di);
     }
 #pragma unroll
-    for (int i = 0; i < NZ; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
-        for (int j = i; j < NZ; ++j) {
+        for (int j = i; j < NA; ++j) {
             double acc = 0.0;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) acc += V[i][k] * d[k] * V[j][k];
+            for (int k = 0; k < NA; ++k) acc += V[i][k] * d[k] * V[j][k];
             A[i][j] = acc;
             A[j][i] = acc;
         }

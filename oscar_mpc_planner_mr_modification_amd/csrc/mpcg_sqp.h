@@ -72,6 +72,11 @@ struct Cfg {
     // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
     static constexpr bool LIN_PARAMS = NS > 0;
     static constexpr int NHS = LIN_PARAMS ? (NE > 0 ? NE : 1) : NH;  // rows with LDS storage
+    // Keep parameter loads inside the SQP / QP loops (no hoisting into long-lived
+    // registers): removes most scratch spills of the long-horizon and slack-model
+    // instances (C4 188 -> 20 B/lane, C5 420 -> 140); C1/C2 fit without it and run
+    // 1 % faster with the hoisted loads.
+    static constexpr bool RELOAD_PARAMS = NS > 0 || N >= 30;
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
     __host__ __device__ static constexpr int blk(int v) {
@@ -122,6 +127,13 @@ struct Lds {
 #define STAMP_LAP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc_[i] += t_ - st_l_; st_l_ = t_; } while (0)
 #define STAMP_STORE(ptr, sol) \
     do { if ((ptr) && threadIdx.x == 0) for (int i_ = 0; i_ < MPCG_NSTAMP; ++i_) (ptr)[(size_t)(sol) * MPCG_NSTAMP + i_] = st_acc_[i_]; } while (0)
+#elif defined(MPCG_MARKERS)
+// assembly markers of the phases (ISA inspection builds only)
+#define STAMP_DECL
+#define STAMP_BEGIN() asm volatile("; @@begin")
+#define STAMP_END(i) asm volatile("; @@end " #i)
+#define STAMP_LAP(i) asm volatile("; @@lap " #i)
+#define STAMP_STORE(ptr, sol) do {} while (0)
 #else
 #define STAMP_DECL
 #define STAMP_BEGIN() do {} while (0)
@@ -348,6 +360,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     double res_eq = 0.0;
 
     for (int it = 0; it < pr.sqp_iters; ++it) {
+        // parameter loads are re-issued where they are used rather than hoisted out of
+        // the SQP / QP loops into registers that stay live (and spill) across them
+        if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
         // =============== preparation: linearise every stage ===============
         STAMP_BEGIN();
         {
@@ -398,17 +413,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // diagonal (quadratic slack cost, linear in every h row, no dynamics
                     // coupling): MIRROR of the 8x8 block = MIRROR of the leading 7x7 block
                     // plus the mirrored slack diagonal, with the same sweep count
-                    double H7[NZ - 1][NZ - 1];
-#pragma unroll
-                    for (int i = 0; i < NZ - 1; ++i)
-#pragma unroll
-                        for (int j = 0; j < NZ - 1; ++j) H7[i][j] = H[i][j];
                     const double hs = H[NZ - 1][NZ - 1];
-                    mirror<NZ - 1>(H7, pr.reg_eps, hs * hs);
-#pragma unroll
-                    for (int i = 0; i < NZ - 1; ++i)
-#pragma unroll
-                        for (int j = 0; j < NZ - 1; ++j) H[i][j] = H7[i][j];
+                    mirror<NZ, NZ - 1>(H, pr.reg_eps, hs * hs);
                     H[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
                 } else {
                     mirror<NZ>(H, pr.reg_eps);
@@ -472,6 +478,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         int qstat = AC_MAXITER, qit = 0;
         double Hdz[NZ];  // part 0: H_k dz_k of the current iterate
         for (;; ++qit) {
+            if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
             // ---- residuals
             STAMP_BEGIN();
             double rs = 0.0, re = 0.0, ri = 0.0, comp = 0.0;
