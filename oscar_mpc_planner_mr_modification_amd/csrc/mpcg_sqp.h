@@ -70,7 +70,10 @@ struct Cfg {
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
     // only the ellipsoid rows keep gradients / gaps in LDS.  Used where it lowers the
     // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
-    static constexpr bool LIN_PARAMS = NS > 0;
+    static constexpr bool LIN_PARAMS = NS > 0 || N >= 30;
+    // gradient components kept per LDS row: with LIN_PARAMS the psi component is
+    // rebuilt from (x, y) components and the stage's disc-offset derivatives
+    static constexpr int DGC = LIN_PARAMS ? 2 : 3;
     static constexpr int NHS = LIN_PARAMS ? (NE > 0 ? NE : 1) : NH;  // rows with LDS storage
     // Keep parameter loads inside the SQP / QP loops (no hoisting into long-lived
     // registers): removes most scratch spills of the long-horizon and slack-model
@@ -108,9 +111,9 @@ struct Lds {
     double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
     double Y[N][NU][NX];      // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
-    double Dg[N][C::NHS][3];  // signed h-row gradients on (x, y, psi); the slack one is C::slack_coef
+    double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
     double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
-    double disc[C::LIN_PARAMS && C::NS > 0 ? N : 1][4];  // scenario rows: off cos psi, off sin psi, d/dpsi of both
+    double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
     double Msc[C::NTRI];      // factorisation scratch
     double xinit[NX];
     int flag;
@@ -203,8 +206,8 @@ struct LaneRows {
 // (xx xy xp yy yp pp on x, y, psi) of the h rows of a lane at stage k.
 template <class C>
 __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[C::NZ],
-                                       const LaneRows<C>& LR, const double* nlam, double hb6[6], double (*Dg)[3],
-                                       double* hd, double* disc) {
+                                       const LaneRows<C>& LR, const double* nlam, double hb6[6],
+                                       double (*Dg)[C::DGC], double* hd, double* disc) {
     const double x = z[2], y = z[3], psi = z[4];
     const double rdisc = C::NE > 0 ? pk[pr.i_disc_r] : 0.0, off = pk[pr.i_disc_off];
     double sp, cp;
@@ -219,12 +222,13 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
         const int hh = LR.hrow(r);
         if (hh < C::NL) {
             // topology halfspace a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370)
-            if constexpr (C::LIN_PARAMS) continue;  // read from the parameters where used
-            const double* c = pk + pr.i_lin0 + 3 * hh;
-            hd[hh] = 0.0 - (c[0] * x + c[1] * y - c[2]);
-            Dg[hh][0] = c[0];
-            Dg[hh][1] = c[1];
-            Dg[hh][2] = 0.0;
+            if constexpr (!C::LIN_PARAMS) {  // else read from the parameters where used
+                const double* c = pk + pr.i_lin0 + 3 * hh;
+                hd[hh] = 0.0 - (c[0] * x + c[1] * y - c[2]);
+                Dg[hh][0] = c[0];
+                Dg[hh][1] = c[1];
+                Dg[hh][2] = 0.0;
+            }
         } else if (hh >= C::NL + C::NE) {
             // scenario halfspace a1 xd + a2 yd - (b + slack) <= 0 at the disc
             // position (scenario_constraints.py:64-94)
@@ -256,7 +260,7 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             hd[he] = (ddx * Mdx + ddy * Mdy) - 1.0;
             Dg[he][0] = -2.0 * Mdx;
             Dg[he][1] = -2.0 * Mdy;
-            Dg[he][2] = -2.0 * (Mdx * dxp + Mdy * dyp);
+            if constexpr (!C::LIN_PARAMS) Dg[he][2] = -2.0 * (Mdx * dxp + Mdy * dyp);
             const double wgt = -nlam[r];  // lower-bound row: Hessian weight -lambda
             if (wgt != 0.0) {
                 const double hxp = 2.0 * (M00 * dxp + M01 * dyp);
@@ -276,6 +280,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
     constexpr int ZS = NU + 5;  // slack variable (NB == 4)
     __shared__ Lds<C> S;
+#ifdef MPCG_LDS_PAD
+    // occupancy experiment only: pad the LDS footprint
+    __shared__ char lds_pad[MPCG_LDS_PAD];
+    if (threadIdx.x == 1000) lds_pad[blockIdx.x % MPCG_LDS_PAD] = 0;
+#endif
     const int sol = blockIdx.x;
     if (sol >= batch) return;
     const int lane = threadIdx.x;
@@ -315,11 +324,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 const double* p = hh < C::NL ? pk + pr.i_lin0 + 3 * hh : pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
                 a = p[0];
                 b = p[1];
-                c = hh < C::NL ? 0.0 : p[0] * S.disc[C::NS > 0 ? k : 0][2] + p[1] * S.disc[C::NS > 0 ? k : 0][3];
+                c = hh < C::NL ? 0.0 : p[0] * S.disc[k][2] + p[1] * S.disc[k][3];
                 return;
             }
             const int he = hh - C::NL;
-            a = S.Dg[k][he][0]; b = S.Dg[k][he][1]; c = S.Dg[k][he][2];
+            a = S.Dg[k][he][0];
+            b = S.Dg[k][he][1];
+            c = a * S.disc[k][2] + b * S.disc[k][3];
         } else {
             a = S.Dg[k][hh][0]; b = S.Dg[k][hh][1]; c = S.Dg[k][hh][2];
         }
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (hh >= C::NL + C::NE) {
                 const double* p = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
                 const double sl = C::NX > 5 ? S.z[k][NU + 5] : 0.0;
-                return 0.0 - (p[0] * (x + S.disc[C::NS > 0 ? k : 0][0]) + p[1] * (y + S.disc[C::NS > 0 ? k : 0][1]) - (p[2] + sl));
+                return 0.0 - (p[0] * (x + S.disc[k][0]) + p[1] * (y + S.disc[k][1]) - (p[2] + sl));
             }
             return S.hd[k][hh - C::NL];
         } else {
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
             double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS && C::NS > 0 ? k : 0]);
+            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
             STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {
