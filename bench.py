@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
-    ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2/C4: 1024, C5: 2048)")
+    ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2: 1024, C4: 2048, C5: 2048)")
     ap.add_argument("--guesses", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -88,7 +88,8 @@ def main():
     lay = config_layout(args.config)
     if args.config == "C5":
         return run_shmpc(args, lay, world, rank, dev)
-    S, G, N = args.scenes or 1024, args.guesses, lay.N
+    # BASELINE.json configs[3]: 16384 scenes over 8 GPUs -> 2048 per GPU for C4
+    S, G, N = args.scenes or (2048 if args.config == "C4" else 1024), args.guesses, lay.N
     B = S * G
     W_CONS, SEL_W = SETTINGS_WEIGHTS["consistency"], 0.75   # guidance_planner.yaml:37 selection weight
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
