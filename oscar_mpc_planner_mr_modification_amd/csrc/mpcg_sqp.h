@@ -903,14 +903,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double ddb[BVS];
 #pragma unroll
                     for (int j = 0; j < BVS; ++j) ddb[j] = LR.box_on(j) ? S.ddz[k][LR.var(j)] : 0.0;
+                    // h rows: D . ddz once per phase (the passes below reuse it)
+                    double ddh[HS];
+#pragma unroll
+                    for (int r = 0; r < HS; ++r) {
+                        double v = 0.0;
+                        if (LR.h_on(r)) {
+                            const int hh = LR.hrow(r);
+                            double ga, gb, gc;
+                            rowg(hh, ga, gb, gc);
+                            v = ga * ddk[2] + gb * ddk[3] + gc * ddk[4];
+                            if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
+                        }
+                        ddh[r] = v;
+                    }
                     auto ddot = [&](int s) {
                         if (s < HB) return (s & 1) ? ddb[s >> 1] : -ddb[s >> 1];
-                        const int hh = LR.hrow(s - HB);
-                        double ga, gb, gc;
-                        rowg(hh, ga, gb, gc);
-                        double v = ga * ddk[2] + gb * ddk[3] + gc * ddk[4];
-                        if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
-                        return v;
+                        return ddh[s - HB];
                     };
                     auto active = [&](int s) { return s < HB ? LR.box_on(s >> 1) : LR.h_on(s - HB); };
                     // dt = -rin - D ddz; dl = -(rc + l dt) / t
