@@ -27,14 +27,20 @@
 extern "C" {
 #endif
 
-/* ContouringSecondOrderUnicycleModel (solver_model.py:185-214): nx 5.  The
+/* ContouringSecondOrderUnicycleModel (solver_model.py:185-214): nx 5, nu 2.  The
  * SH-MPC model ContouringSecondOrderUnicycleModelWithSlack (:274-298) adds the
- * slack state last: nx 6.  Every buffer below is sized by mpcg_problem.nx. */
+ * slack state last: nx 6.  BicycleModel2ndOrderCurvatureAware (:355-437, C3):
+ * nu 3 (a, w, slack), nx 6 (x, y, psi, v, delta, spline).  Every buffer below is
+ * sized by mpcg_problem.nx / nu. */
 #define MPCG_NX 5
 #define MPCG_MAX_NX 6
-#define MPCG_NU 2
+#define MPCG_NU 2            /* the unicycle models */
+#define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 3
+#define MPCG_ABI_VERSION 4
+/* mpcg_problem.model */
+#define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
+#define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
 
 /* Problem description: the generated solver's dimensions + the parameter
  * map (parameter_map.yaml written by solver_generator/generate_solver.py:34-46)
@@ -51,18 +57,25 @@ typedef struct mpcg_problem {
     int i_disc_r, i_disc_off;
     int i_ell0;                    /* obstacle j at i_ell0 + 7 j: x y psi major minor chi r */
     int n_scen, i_scen0;           /* scenario halfspace i at i_scen0 + 3 i: a1 a2 b
-                                      (a1 xd + a2 yd - (b + slack) <= 0, scenario_constraints.py:64-94) */
-    int i_w_slack;                 /* MPCBase weight of the slack state (nx 6) */
-    int nx;                        /* 5, or 6 with the slack state */
+                                      (a1 xd + a2 yd - (b + slack) <= 0, scenario_constraints.py:64-94);
+                                      the bicycle model: the decomp halfspaces, same row
+                                      (disc_0_decomp_<i>_a1 ..., decomp_constraints.py:46-98) */
+    int i_w_slack;                 /* MPCBase weight of the slack variable */
+    int nx;                        /* 5, or 6 with the slack state / the bicycle */
     double dt;                     /* integrator_step; ERK4 over dt with rk_steps steps */
-    int rk_steps;
-    double lbu[MPCG_NU], ubu[MPCG_NU], lbx[MPCG_MAX_NX], ubx[MPCG_MAX_NX];
+    int rk_steps;                  /* acados sim_method_num_steps 3; the bicycle (Forces RK4): 1 */
+    double lbu[MPCG_MAX_NU], ubu[MPCG_MAX_NU], lbx[MPCG_MAX_NX], ubx[MPCG_MAX_NX];
     int sqp_iters;                 /* solver_settings.acados.iterations (timeout disabled) */
     double qp_tol;                 /* 1e-5 */
     int qp_iter_max;               /* 50 */
     double reg_eps;                /* MIRROR epsilon 1e-4 */
     double qp_mu0, qp_thr0;        /* interior-point cold start */
     double res_eq_fail;            /* 1e-2 */
+    int nu;                        /* 2, or 3 for the bicycle */
+    int model;                     /* MPCG_MODEL_* */
+    int i_w_tangle, i_w_tcont;     /* terminal_angle / terminal_contouring: read by the bicycle model's
+                                      CurvatureAwareContouring at stage N-1 (curvature_aware_contouring.py:94-103,
+                                      Forces' per-stage objective, generate_forces_solver.py:50-59) */
 } mpcg_problem;
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,
@@ -92,6 +105,14 @@ int mpcg_lam_size(const mpcg_problem *pr);
 int mpcg_problem_from_map(mpcg_problem *pr, int N, int nx, int npar, int n_entries, const char *const *names,
                           const int *indices, const double *lb, const double *ub, double dt,
                           int sqp_iters);
+
+/* Same for a given model (MPCG_MODEL_*): the bicycle (nx 6, nu 3) finds its
+ * decomp halfspaces by `disc_0_decomp_<i>_a1`, the terminal weights by
+ * "terminal_angle" / "terminal_contouring", and integrates with one RK4 step
+ * (rk_steps 1); lb/ub hold nu + nx bounds. */
+int mpcg_problem_from_map_model(mpcg_problem *pr, int model, int N, int nx, int npar, int n_entries,
+                                const char *const *names, const int *indices, const double *lb, const double *ub,
+                                double dt, int sqp_iters);
 
 /* Input/output buffers of one batched solve (all device pointers for
  * mpcg_solve, all host pointers for mpcg_context_solve).
@@ -232,7 +253,7 @@ int mpcg_advance(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg
                  unsigned char *consistency_on_next, unsigned char *previously_selected_next, double *lam_next,
                  void *stream);
 
-/* 0 if (N, nx, n_lin, n_ell, n_scen) has a compiled kernel instance, else -1 */
+/* 0 if (model, N, nx, n_lin, n_ell, n_scen) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);
 
 /* Batched solve, every pointer in device memory, enqueued on `stream`

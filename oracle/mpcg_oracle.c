@@ -30,6 +30,7 @@ enum { AC_SUCCESS = 0, AC_NAN = 1, AC_MAXITER = 2, AC_MINSTEP = 3, AC_QP_FAILURE
 /* Glued cubic spline (spline.py:4-86)                                 */
 /* ------------------------------------------------------------------ */
 
+#ifndef ORC_BICYCLE_CA
 /* value and first two s-derivatives of the sigmoid glue weight
  * lambda_k(s) = 1 / (1 + exp((s - s_k + 0.02) / 0.1))        (spline.py:37) */
 static void glue_weight(double s, double sk, double *l0, double *l1, double *l2) {
@@ -71,6 +72,29 @@ static void spline_axis(const orc_problem *pr, const double *p, double s, int ax
     }
     memcpy(G, V, sizeof V);
     memcpy(D, W, sizeof W);
+}
+
+#endif
+
+#ifdef ORC_BICYCLE_CA
+#define SLACK_IDX 2 /* the slack input of BicycleModel2ndOrderCurvatureAware (solver_model.py:364) */
+#else
+#define SLACK_IDX (NU + NX - 1)
+#endif
+
+#ifdef ORC_BICYCLE_CA
+#include "orc_bicycle_ca.inc"
+#else
+void orc_ca_update(const orc_problem *pr, const double *z, const double *I, const double *p,
+                   double *g, double *grad, double *hess) {
+    (void)pr; (void)z; (void)I; (void)p; (void)grad; (void)hess;
+    *g = 0.0;
+}
+
+void orc_stage_cost_k(const orc_problem *pr, int k, const double *z, const double *p,
+                      double *Lout, double *grad, double *hess) {
+    (void)k;
+    orc_stage_cost(pr, z, p, Lout, grad, hess);
 }
 
 /* ------------------------------------------------------------------ */
@@ -154,10 +178,13 @@ void orc_stage_cost(const orc_problem *pr, const double *z, const double *p,
     if (hess) memcpy(hess, H, sizeof H);
 }
 
+#endif /* ORC_BICYCLE_CA */
+
 /* ------------------------------------------------------------------ */
 /* Constraints h(z) (solver_definition.py:37-49)                      */
 /* ------------------------------------------------------------------ */
 int orc_nx(void) { return ORC_NX; }
+int orc_nu(void) { return ORC_NU; }
 
 int orc_num_h(const orc_problem *pr) { return pr->n_lin + pr->n_ell + pr->n_scen; }
 
@@ -172,15 +199,15 @@ void orc_h_bounds(const orc_problem *pr, double *lh, double *uh) {
 void orc_stage_constraints(const orc_problem *pr, const double *z, const double *p,
                            double *h, double *jac, double *hess) {
     int nh = orc_num_h(pr);
-    double x = z[2], y = z[3], psi = z[4];
+    double x = z[NU + 0], y = z[NU + 1], psi = z[NU + 2];
     memset(jac, 0, sizeof(double) * nh * NZ);
     if (hess) memset(hess, 0, sizeof(double) * nh * NZ * NZ);
     /* topology halfspaces a1 x + a2 y - b <= 0 (guidance_constraints.py:355-370) */
     for (int i = 0; i < pr->n_lin; i++) {
         const double *c = p + pr->i_lin0 + 3 * i;
         h[i] = c[0] * x + c[1] * y - c[2];
-        jac[i * NZ + 2] = c[0];
-        jac[i * NZ + 3] = c[1];
+        jac[i * NZ + NU + 0] = c[0];
+        jac[i * NZ + NU + 1] = c[1];
     }
     /* obstacle ellipsoids d' R' D R d >= 1 (ellipsoid_constraints.py:435-489), one disc */
     double rd = pr->i_disc_r >= 0 ? p[pr->i_disc_r] : 0.0, off = pr->i_disc_off >= 0 ? p[pr->i_disc_off] : 0.0;
@@ -202,36 +229,38 @@ void orc_stage_constraints(const orc_problem *pr, const double *z, const double 
         double Mdx = M00 * dx + M01 * dy, Mdy = M01 * dx + M11 * dy;
         int r = pr->n_lin + j;
         h[r] = dx * Mdx + dy * Mdy;
-        jac[r * NZ + 2] = 2.0 * Mdx;
-        jac[r * NZ + 3] = 2.0 * Mdy;
-        jac[r * NZ + 4] = 2.0 * (Mdx * dxp + Mdy * dyp);
+        jac[r * NZ + NU + 0] = 2.0 * Mdx;
+        jac[r * NZ + NU + 1] = 2.0 * Mdy;
+        jac[r * NZ + NU + 2] = 2.0 * (Mdx * dxp + Mdy * dyp);
         if (hess) {
             double *Hr = hess + (size_t)r * NZ * NZ;
-            Hr[2 * NZ + 2] = 2.0 * M00; Hr[2 * NZ + 3] = 2.0 * M01;
-            Hr[3 * NZ + 2] = 2.0 * M01; Hr[3 * NZ + 3] = 2.0 * M11;
+            Hr[(NU + 0) * NZ + NU + 0] = 2.0 * M00; Hr[(NU + 0) * NZ + NU + 1] = 2.0 * M01;
+            Hr[(NU + 1) * NZ + NU + 0] = 2.0 * M01; Hr[(NU + 1) * NZ + NU + 1] = 2.0 * M11;
             double hxp = 2.0 * (M00 * dxp + M01 * dyp);
             double hyp = 2.0 * (M01 * dxp + M11 * dyp);
-            Hr[2 * NZ + 4] = hxp; Hr[4 * NZ + 2] = hxp;
-            Hr[3 * NZ + 4] = hyp; Hr[4 * NZ + 3] = hyp;
-            Hr[4 * NZ + 4] = 2.0 * (dxp * (M00 * dxp + M01 * dyp) + dyp * (M01 * dxp + M11 * dyp)) +
+            Hr[(NU + 0) * NZ + NU + 2] = hxp; Hr[(NU + 2) * NZ + NU + 0] = hxp;
+            Hr[(NU + 1) * NZ + NU + 2] = hyp; Hr[(NU + 2) * NZ + NU + 1] = hyp;
+            Hr[(NU + 2) * NZ + NU + 2] = 2.0 * (dxp * (M00 * dxp + M01 * dyp) + dyp * (M01 * dxp + M11 * dyp)) +
                              2.0 * (Mdx * dxpp + Mdy * dypp);
         }
     }
     /* scenario halfspaces a1 xd + a2 yd - (b + slack) <= 0 at the disc position
-     * (x, y) + R(psi) (offset, 0) (scenario_constraints.py:64-94) */
+     * (x, y) + R(psi) (offset, 0) (scenario_constraints.py:64-94); C3: the decomp
+     * halfspaces, same formula (decomp_constraints.py:68-98) */
     for (int i = 0; i < pr->n_scen; i++) {
         const double *c = p + pr->i_scen0 + 3 * i;
         int r = pr->n_lin + pr->n_ell + i;
-        double sl = (NX > 5) ? z[NU + NX - 1] : 0.0;
+        double sl = (NX > 5) ? z[SLACK_IDX] : 0.0;
         h[r] = c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl);
-        jac[r * NZ + 2] = c[0];
-        jac[r * NZ + 3] = c[1];
-        jac[r * NZ + 4] = c[0] * dxp + c[1] * dyp;
-        if (NX > 5) jac[r * NZ + NU + NX - 1] = -1.0;
-        if (hess) hess[(size_t)r * NZ * NZ + 4 * NZ + 4] = c[0] * dxpp + c[1] * dypp;
+        jac[r * NZ + NU + 0] = c[0];
+        jac[r * NZ + NU + 1] = c[1];
+        jac[r * NZ + NU + 2] = c[0] * dxp + c[1] * dyp;
+        if (NX > 5) jac[r * NZ + SLACK_IDX] = -1.0;
+        if (hess) hess[(size_t)r * NZ * NZ + (NU + 2) * NZ + NU + 2] = c[0] * dxpp + c[1] * dypp;
     }
 }
 
+#ifndef ORC_BICYCLE_CA
 /* ------------------------------------------------------------------ */
 /* Dynamics (solver_model.py:207-214)                                  */
 /* ------------------------------------------------------------------ */
@@ -257,99 +286,139 @@ void orc_dynamics(const double *z, double *f, double *jac, double *hess) {
     }
 }
 
+#endif
+
 /* ------------------------------------------------------------------ */
 /* acados ERK (4 stages, rk_steps steps) with forward sensitivities and */
 /* the exact second-order adjoint (generate_acados_solver.py:148-150,   */
 /* hessian_approx EXACT :155)                                           */
 /* ------------------------------------------------------------------ */
 #define ORC_MAX_EVAL 64
-void orc_erk4(const orc_problem *pr, const double *z, double *xnext, double *A, double *B,
-              const double *adj, double *hess) {
+#define NXI ORC_NXI
+/* ERK over the NXI integrated states (all of them except C3's spline state,
+ * do_not_use_integration_for_last_n_states, solver_model.py:66-78, 366);
+ * C3 then applies the CA spline update (model_discrete_dynamics) on top.
+ * p: the stage parameters (read by the C3 update only, may be NULL otherwise). */
+void orc_discrete(const orc_problem *pr, const double *z, const double *p, double *xnext, double *A,
+                  double *B, const double *adj, double *hess) {
     int ns = pr->rk_steps;
     double h = pr->dt / ns;
-    double y[NX], S[NX][NZ];
+    double y[NXI], S[NXI][NZ];
     static const double cst[4] = {0.0, 0.5, 0.5, 1.0};
     static const double wgt[4] = {1.0 / 6.0, 2.0 / 6.0, 2.0 / 6.0, 1.0 / 6.0};
     double W[ORC_MAX_EVAL][NZ];           /* f argument (z-order) of each evaluation */
-    double Se[ORC_MAX_EVAL][NX][NZ];      /* d(state argument)/dz */
-    double Je[ORC_MAX_EVAL][NX][NZ];      /* df/dz' at the argument */
-    for (int i = 0; i < NX; i++) {
+    double Se[ORC_MAX_EVAL][NXI][NZ];     /* d(integrated state argument)/dz */
+    double Je[ORC_MAX_EVAL][NXI][NZ];     /* df/dz' at the argument */
+    for (int i = 0; i < NXI; i++) {
         y[i] = z[NU + i];
         for (int j = 0; j < NZ; j++) S[i][j] = (j == NU + i) ? 1.0 : 0.0;
     }
     int e = 0;
     for (int st = 0; st < ns; st++) {
-        double k[4][NX], dk[4][NX][NZ];
+        double k[4][NXI], dk[4][NXI][NZ];
         for (int q = 0; q < 4; q++, e++) {
-            /* argument y + c_q h k_{q-1} */
-            W[e][0] = z[0]; W[e][1] = z[1];
-            for (int i = 0; i < NX; i++) {
+            /* argument y + c_q h k_{q-1}; inputs and non-integrated states held */
+            for (int i = 0; i < NU; i++) W[e][i] = z[i];
+            for (int i = NXI; i < NX; i++) W[e][NU + i] = z[NU + i];
+            for (int i = 0; i < NXI; i++) {
                 W[e][NU + i] = y[i] + (q ? cst[q] * h * k[q - 1][i] : 0.0);
                 for (int j = 0; j < NZ; j++)
                     Se[e][i][j] = S[i][j] + (q ? cst[q] * h * dk[q - 1][i][j] : 0.0);
             }
-            double J[NX * NZ];
+            double J[NXI * NZ];
             orc_dynamics(W[e], k[q], J, NULL);
-            for (int i = 0; i < NX; i++)
+            for (int i = 0; i < NXI; i++)
                 for (int j = 0; j < NZ; j++) Je[e][i][j] = J[i * NZ + j];
-            /* dk = Jx * Se + Ju * [I 0] */
-            for (int i = 0; i < NX; i++)
+            /* dk = Jx * Se + Ju * [I 0] (+ the held states' columns) */
+            for (int i = 0; i < NXI; i++)
                 for (int j = 0; j < NZ; j++) {
                     double acc = (j < NU) ? J[i * NZ + j] : 0.0;
-                    for (int m = 0; m < NX; m++) acc += J[i * NZ + NU + m] * Se[e][m][j];
+                    for (int m = 0; m < NXI; m++) acc += J[i * NZ + NU + m] * Se[e][m][j];
+                    for (int m = NXI; m < NX; m++) acc += (j == NU + m) ? J[i * NZ + NU + m] : 0.0;
                     dk[q][i][j] = acc;
                 }
         }
-        for (int i = 0; i < NX; i++) {
+        for (int i = 0; i < NXI; i++) {
             y[i] += h * (wgt[0] * k[0][i] + wgt[1] * k[1][i] + wgt[2] * k[2][i] + wgt[3] * k[3][i]);
             for (int j = 0; j < NZ; j++)
                 S[i][j] += h * (wgt[0] * dk[0][i][j] + wgt[1] * dk[1][i][j] + wgt[2] * dk[2][i][j] + wgt[3] * dk[3][i][j]);
         }
     }
-    for (int i = 0; i < NX; i++) {
+    for (int i = 0; i < NXI; i++) {
         xnext[i] = y[i];
         for (int j = 0; j < NX; j++) A[i * NX + j] = S[i][NU + j];
         for (int j = 0; j < NU; j++) B[i * NU + j] = S[i][j];
     }
+    double yb[NXI];
+    for (int i = 0; i < NXI; i++) yb[i] = adj ? adj[i] : 0.0;
+#ifdef ORC_BICYCLE_CA
+    /* the CA spline update g(z, I) at I = the integrated states (solver_model.py:409-437) */
+    enum { NG = NZ + NXI };
+    double gv, gg[NG], gh[NG * NG];
+    orc_ca_update(pr, z, y, p, &gv, gg, (adj && hess) ? gh : NULL);
+    xnext[NX - 1] = gv;
+    for (int j = 0; j < NZ; j++) {
+        double acc = gg[j];
+        for (int i = 0; i < NXI; i++) acc += gg[NZ + i] * S[i][j];
+        if (j < NU) B[(NX - 1) * NU + j] = acc;
+        else A[(NX - 1) * NX + j - NU] = acc;
+    }
+    /* the update's own adjoint flows into the integrated states */
+    if (adj)
+        for (int i = 0; i < NXI; i++) yb[i] += adj[NX - 1] * gg[NZ + i];
+#endif
     if (!adj || !hess) return;
-    /* reverse sweep: ybar = adjoint of the step output; kbar_q = adjoint of k_q */
-    double yb[NX];
-    memcpy(yb, adj, sizeof yb);
     memset(hess, 0, sizeof(double) * NZ * NZ);
+#ifdef ORC_BICYCLE_CA
+    /* adj_s * Wg' Hess(g) Wg, Wg = d(z, I)/dz = [I_nz; S] */
+    {
+        double Wg[NG][NZ];
+        for (int r = 0; r < NG; r++)
+            for (int j = 0; j < NZ; j++) Wg[r][j] = r < NZ ? (r == j ? 1.0 : 0.0) : S[r - NZ][j];
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NZ; j++) {
+                double acc = 0.0;
+                for (int m = 0; m < NG; m++)
+                    for (int n = 0; n < NG; n++) acc += Wg[m][i] * gh[m * NG + n] * Wg[n][j];
+                hess[i * NZ + j] += adj[NX - 1] * acc;
+            }
+    }
+#endif
+    /* reverse sweep: ybar = adjoint of the step output; kbar_q = adjoint of k_q */
     for (int st = ns - 1; st >= 0; st--) {
-        double kb[4][NX];
+        double kb[4][NXI];
         int e0 = 4 * st;
         for (int q = 3; q >= 0; q--) {
-            for (int i = 0; i < NX; i++) kb[q][i] = h * wgt[q] * yb[i];
+            for (int i = 0; i < NXI; i++) kb[q][i] = h * wgt[q] * yb[i];
             if (q < 3) { /* k_q feeds the argument of k_{q+1} with factor c_{q+1} h */
-                for (int i = 0; i < NX; i++) {
+                for (int i = 0; i < NXI; i++) {
                     double acc = 0.0;
-                    for (int m = 0; m < NX; m++) acc += Je[e0 + q + 1][m][NU + i] * kb[q + 1][m];
+                    for (int m = 0; m < NXI; m++) acc += Je[e0 + q + 1][m][NU + i] * kb[q + 1][m];
                     kb[q][i] += cst[q + 1] * h * acc;
                 }
             }
         }
-        double ybn[NX];
-        for (int i = 0; i < NX; i++) {
+        double ybn[NXI];
+        for (int i = 0; i < NXI; i++) {
             double acc = yb[i];
             for (int q = 0; q < 4; q++)
-                for (int m = 0; m < NX; m++) acc += Je[e0 + q][m][NU + i] * kb[q][m];
+                for (int m = 0; m < NXI; m++) acc += Je[e0 + q][m][NU + i] * kb[q][m];
             ybn[i] = acc;
         }
-        /* second-order terms: sum_q We' Hess(kbar_q' f) We, We = d[u; y_arg]/dz */
+        /* second-order terms: sum_q We' Hess(kbar_q' f) We, We = d[u; y_arg; held]/dz */
         for (int q = 0; q < 4; q++) {
             int ee = e0 + q;
-            double Hf[NX * NZ * NZ], f[NX], Hm[NZ][NZ], Wm[NZ][NZ];
+            double Hf[NXI * NZ * NZ], f[NXI], Hm[NZ][NZ], Wm[NZ][NZ];
             orc_dynamics(W[ee], f, NULL, Hf);
             for (int i = 0; i < NZ; i++)
                 for (int j = 0; j < NZ; j++) {
                     double acc = 0.0;
-                    for (int m = 0; m < NX; m++) acc += kb[q][m] * Hf[m * NZ * NZ + i * NZ + j];
+                    for (int m = 0; m < NXI; m++) acc += kb[q][m] * Hf[m * NZ * NZ + i * NZ + j];
                     Hm[i][j] = acc;
                 }
             for (int i = 0; i < NZ; i++)
                 for (int j = 0; j < NZ; j++)
-                    Wm[i][j] = (i < NU) ? (i == j ? 1.0 : 0.0) : Se[ee][i - NU][j];
+                    Wm[i][j] = (i < NU || i - NU >= NXI) ? (i == j ? 1.0 : 0.0) : Se[ee][i - NU][j];
             for (int i = 0; i < NZ; i++)
                 for (int j = 0; j < NZ; j++) {
                     double acc = 0.0;
@@ -360,6 +429,11 @@ void orc_erk4(const orc_problem *pr, const double *z, double *xnext, double *A, 
         }
         memcpy(yb, ybn, sizeof yb);
     }
+}
+
+void orc_erk4(const orc_problem *pr, const double *z, double *xnext, double *A, double *B,
+              const double *adj, double *hess) {
+    orc_discrete(pr, z, NULL, xnext, A, B, adj, hess);
 }
 
 /* ------------------------------------------------------------------ */
@@ -528,24 +602,33 @@ static int riccati_factor(qp_ws *w) {
                 for (int m = 0; m < NX; m++) acc += F[m][i] * PF[m][j];
                 M[i][j] = acc;
             }
-        /* Cholesky of Muu */
-        double l00 = M[0][0];
-        if (!(l00 > 0.0)) return -1;
-        l00 = sqrt(l00);
-        double l10 = M[1][0] / l00;
-        double l11 = M[1][1] - l10 * l10;
-        if (!(l11 > 0.0)) return -1;
-        l11 = sqrt(l11);
-        S->L[0][0] = l00; S->L[0][1] = 0.0; S->L[1][0] = l10; S->L[1][1] = l11;
-        /* Y = L^{-1} Mux */
-        for (int j = 0; j < NX; j++) {
-            double y0 = M[0][NU + j] / l00;
-            double y1 = (M[1][NU + j] - l10 * y0) / l11;
-            S->Y[0][j] = y0; S->Y[1][j] = y1;
+        /* Cholesky of Muu (L L' = Muu) */
+        for (int j = 0; j < NU; j++) {
+            double d = M[j][j];
+            for (int m = 0; m < j; m++) d -= S->L[j][m] * S->L[j][m];
+            if (!(d > 0.0)) return -1;
+            d = sqrt(d);
+            S->L[j][j] = d;
+            for (int i = j + 1; i < NU; i++) {
+                double acc = M[i][j];
+                for (int m = 0; m < j; m++) acc -= S->L[i][m] * S->L[j][m];
+                S->L[i][j] = acc / d;
+            }
+            for (int i = 0; i < j; i++) S->L[i][j] = 0.0;
         }
+        /* Y = L^{-1} Mux */
+        for (int j = 0; j < NX; j++)
+            for (int i = 0; i < NU; i++) {
+                double acc = M[i][NU + j];
+                for (int m = 0; m < i; m++) acc -= S->L[i][m] * S->Y[m][j];
+                S->Y[i][j] = acc / S->L[i][i];
+            }
         for (int i = 0; i < NX; i++)
-            for (int j = 0; j < NX; j++)
-                S->P[i][j] = M[NU + i][NU + j] - S->Y[0][i] * S->Y[0][j] - S->Y[1][i] * S->Y[1][j];
+            for (int j = 0; j < NX; j++) {
+                double acc = M[NU + i][NU + j];
+                for (int m = 0; m < NU; m++) acc -= S->Y[m][i] * S->Y[m][j];
+                S->P[i][j] = acc;
+            }
     }
     return 0;
 }
@@ -572,26 +655,38 @@ static void riccati_solve(qp_ws *w) {
             for (int j = 0; j < NX; j++) acc += (i < NU ? S->B[j][i] : S->A[j][i - NU]) * v[j];
             m[i] = acc;
         }
-        double y0 = m[0] / S->L[0][0];
-        double y1 = (m[1] - S->L[1][0] * y0) / S->L[1][1];
-        S->y[0] = y0; S->y[1] = y1;
-        for (int i = 0; i < NX; i++) S->p[i] = m[NU + i] - S->Y[0][i] * y0 - S->Y[1][i] * y1;
+        for (int i = 0; i < NU; i++) { /* y = L^{-1} m_u */
+            double acc = m[i];
+            for (int q = 0; q < i; q++) acc -= S->L[i][q] * S->y[q];
+            S->y[i] = acc / S->L[i][i];
+        }
+        for (int i = 0; i < NX; i++) {
+            double acc = m[NU + i];
+            for (int q = 0; q < NU; q++) acc -= S->Y[q][i] * S->y[q];
+            S->p[i] = acc;
+        }
     }
     /* forward */
     double dx[NX] = {0};
     for (int k = 0; k < N; k++) {
         qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
         /* du = -L^{-T} (Y dx + y) */
-        double c0 = S->y[0], c1 = S->y[1];
-        for (int j = 0; j < NX; j++) { c0 += S->Y[0][j] * dx[j]; c1 += S->Y[1][j] * dx[j]; }
-        /* L^T du = -c  => [l00 l10; 0 l11] du = -c */
-        double du1 = -c1 / S->L[1][1];
-        double du0 = (-c0 - S->L[1][0] * du1) / S->L[0][0];
-        S->ddz[0] = du0; S->ddz[1] = du1;
+        double c[NU], du[NU];
+        for (int i = 0; i < NU; i++) {
+            c[i] = S->y[i];
+            for (int j = 0; j < NX; j++) c[i] += S->Y[i][j] * dx[j];
+        }
+        for (int i = NU - 1; i >= 0; i--) { /* L' du = -c */
+            double acc = -c[i];
+            for (int q = i + 1; q < NU; q++) acc -= S->L[q][i] * du[q];
+            du[i] = acc / S->L[i][i];
+        }
+        for (int i = 0; i < NU; i++) S->ddz[i] = du[i];
         for (int i = 0; i < NX; i++) S->ddz[NU + i] = (k == 0) ? 0.0 : dx[i];
         double dxn[NX];
         for (int i = 0; i < NX; i++) {
-            double acc = r[k][i] + S->B[i][0] * du0 + S->B[i][1] * du1;
+            double acc = r[k][i];
+            for (int j = 0; j < NU; j++) acc += S->B[i][j] * du[j];
             for (int j = 0; j < NX; j++) acc += S->A[i][j] * dx[j];
             dxn[i] = acc;
         }
@@ -602,7 +697,7 @@ static void riccati_solve(qp_ws *w) {
         }
         memcpy(dx, dxn, sizeof dx);
     }
-    SN->ddz[0] = SN->ddz[1] = 0.0;
+    for (int i = 0; i < NU; i++) SN->ddz[i] = 0.0;
     for (int i = 0; i < NX; i++) SN->ddz[NU + i] = dx[i];
 }
 
@@ -802,8 +897,8 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
             qp_stage *S = &w.st[k];
             const double *p = params + (size_t)k * npar;
             double L, g[NZ], Hc[NZ * NZ], Hd[NZ * NZ], xn[NX], A[NX * NX], B[NX * NU];
-            orc_stage_cost(pr, z[k], p, &L, g, Hc);
-            orc_erk4(pr, z[k], xn, A, B, pi[k], Hd);
+            orc_stage_cost_k(pr, k, z[k], p, &L, g, Hc);
+            orc_discrete(pr, z[k], p, xn, A, B, pi[k], Hd);
             for (int i = 0; i < NZ; i++) {
                 S->g[i] = g[i];
                 for (int j = 0; j < NZ; j++) S->H[i][j] = Hc[i * NZ + j] + Hd[i * NZ + j];
@@ -898,7 +993,7 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
     double pobj = 0.0;
     for (int k = 0; k < N; k++) {
         double L;
-        orc_stage_cost(pr, z[k], params + (size_t)k * npar, &L, NULL, NULL);
+        orc_stage_cost_k(pr, k, z[k], params + (size_t)k * npar, &L, NULL, NULL);
         pobj += L;
     }
     for (int k = 0; k <= N; k++)

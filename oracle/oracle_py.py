@@ -1,5 +1,6 @@
 """ctypes binding of the CPU oracle (oracle/libmpcg_oracle.so, nx 5;
-oracle/libmpcg_oracle_slack.so, nx 6 — the C5 slack model).
+oracle/libmpcg_oracle_slack.so, nx 6 — the C5 slack model;
+oracle/libmpcg_oracle_bicycle.so, nu 3 / nx 6 — the C3 curvature-aware bicycle).
 
 TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
 bench.py's cpu_baseline leg, never by the product package.
@@ -15,9 +16,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libmpcg_oracle.so")
 LIB_SLACK = os.path.join(HERE, "libmpcg_oracle_slack.so")
-LIBS = {5: LIB, 6: LIB_SLACK}
+LIB_BICYCLE = os.path.join(HERE, "libmpcg_oracle_bicycle.so")
+LIBS = {"unicycle": LIB, "unicycle_slack": LIB_SLACK, "bicycle_ca": LIB_BICYCLE}
+MODEL_DIMS = {"unicycle": (5, 2), "unicycle_slack": (6, 2), "bicycle_ca": (6, 3)}
 
-ORC_NU, ORC_MAX_NX = 2, 6
+ORC_MAX_NU, ORC_MAX_NX = 3, 6
 
 
 class OrcProblem(C.Structure):
@@ -33,11 +36,12 @@ class OrcProblem(C.Structure):
         ("i_ell0", C.c_int),
         ("n_scen", C.c_int), ("i_scen0", C.c_int), ("i_w_slack", C.c_int), ("nx", C.c_int),
         ("dt", C.c_double), ("rk_steps", C.c_int),
-        ("lbu", C.c_double * 2), ("ubu", C.c_double * 2),
+        ("lbu", C.c_double * ORC_MAX_NU), ("ubu", C.c_double * ORC_MAX_NU),
         ("lbx", C.c_double * ORC_MAX_NX), ("ubx", C.c_double * ORC_MAX_NX),
         ("sqp_iters", C.c_int), ("qp_tol", C.c_double), ("qp_iter_max", C.c_int),
         ("reg_eps", C.c_double), ("qp_mu0", C.c_double), ("qp_thr0", C.c_double),
         ("res_eq_fail", C.c_double),
+        ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int), ("nu", C.c_int),
     ]
 
 
@@ -47,7 +51,7 @@ class OrcInfo(C.Structure):
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("mpcg_oracle.c", "mpcg_oracle.h")]
+    srcs = [os.path.join(HERE, f) for f in ("mpcg_oracle.c", "mpcg_oracle.h", "orc_bicycle_ca.inc", "Makefile")]
     newest = max(os.path.getmtime(f) for f in srcs)
     if force or any(not os.path.exists(x) or os.path.getmtime(x) < newest for x in LIBS.values()):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
@@ -57,9 +61,11 @@ def build(force: bool = False) -> str:
 _libs = {}
 
 
-def lib(nx: int = 5):
-    if nx not in _libs:
-        path = LIBS[nx]
+def lib(model: str = "unicycle"):
+    if isinstance(model, int):  # legacy: nx 5 / 6 of the unicycle models
+        model = "unicycle" if model == 5 else "unicycle_slack"
+    if model not in _libs:
+        path = LIBS[model]
         if not os.path.exists(path):
             build()
         L = C.CDLL(path)
@@ -73,6 +79,9 @@ def lib(nx: int = 5):
         L.orc_h_bounds.argtypes = [P, dp, dp]
         L.orc_dynamics.argtypes = [dp, dp, dp, dp]
         L.orc_erk4.argtypes = [P, dp, dp, dp, dp, C.c_void_p, C.c_void_p]
+        L.orc_discrete.argtypes = [P, dp, C.c_void_p, dp, dp, dp, C.c_void_p, C.c_void_p]
+        L.orc_stage_cost_k.argtypes = [P, C.c_int, dp, dp, dp, dp, dp]
+        L.orc_ca_update.argtypes = [P, dp, dp, dp, dp, dp, dp]
         L.orc_mirror.argtypes = [C.c_int, dp, C.c_double]
         L.orc_solve.argtypes = [P, dp, dp, dp, dp, dp, C.POINTER(OrcInfo)]
         L.orc_solve.restype = C.c_int
@@ -80,10 +89,11 @@ def lib(nx: int = 5):
         vp = C.c_void_p
         L.orc_solve_batch_ex.argtypes = [P, C.c_int, dp, dp, dp, vp, dp, dp, dp, ip, ip, vp, C.c_int]
         L.orc_nx.restype = C.c_int
-        if L.orc_nx() != nx:
-            raise RuntimeError(f"{path} is built for nx={L.orc_nx()}, expected {nx}")
-        _libs[nx] = L
-    return _libs[nx]
+        L.orc_nu.restype = C.c_int
+        if (L.orc_nx(), L.orc_nu()) != MODEL_DIMS[model]:
+            raise RuntimeError(f"{path} is built for nx={L.orc_nx()} nu={L.orc_nu()}, expected {MODEL_DIMS[model]}")
+        _libs[model] = L
+    return _libs[model]
 
 
 def problem_from_layout(layout, **opts) -> OrcProblem:
@@ -98,12 +108,13 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.rk_steps = opts.get("rk_steps", layout.rk_steps)
     pr.n_scen = getattr(layout, "n_scen", 0)
     pr.nx = nx = layout.nx
+    pr.nu = nu = layout.nu
     lb = opts.get("lb", layout.lb)
     ub = opts.get("ub", layout.ub)
-    for i in range(2):
+    for i in range(nu):
         pr.lbu[i], pr.ubu[i] = lb[i], ub[i]
     for i in range(nx):
-        pr.lbx[i], pr.ubx[i] = lb[2 + i], ub[2 + i]
+        pr.lbx[i], pr.ubx[i] = lb[nu + i], ub[nu + i]
     pr.sqp_iters = opts.get("sqp_iters", layout.sqp_iters)
     pr.qp_tol = opts.get("qp_tol", 1e-5)
     pr.qp_iter_max = opts.get("qp_iter_max", 50)
@@ -121,8 +132,9 @@ class Oracle:
         self.layout = layout
         self.pr = problem_from_layout(layout, **opts)
         self.nx = nx = layout.nx
-        self.nz = nx + ORC_NU
-        self.L = lib(nx)
+        self.nu = layout.nu
+        self.nz = nx + self.nu
+        self.L = lib(layout.model)
 
     @property
     def nh(self):
@@ -135,6 +147,34 @@ class Oracle:
         H = np.zeros(nz * nz)
         self.L.orc_stage_cost(C.byref(self.pr), np.ascontiguousarray(z, float), np.ascontiguousarray(p, float), out, g, H)
         return out[0], g, H.reshape(nz, nz)
+
+    def stage_cost_k(self, k, z, p):
+        nz = self.nz
+        out, g, H = np.zeros(1), np.zeros(nz), np.zeros(nz * nz)
+        self.L.orc_stage_cost_k(C.byref(self.pr), k, np.ascontiguousarray(z, float), np.ascontiguousarray(p, float),
+                                out, g, H)
+        return out[0], g, H.reshape(nz, nz)
+
+    def ca_update(self, z, I, p):
+        """C3 CA spline update g(z, I); gradient / Hessian over (z, I)."""
+        n = self.nz + 5
+        out, g, H = np.zeros(1), np.zeros(n), np.zeros(n * n)
+        self.L.orc_ca_update(C.byref(self.pr), np.ascontiguousarray(z, float), np.ascontiguousarray(I, float),
+                             np.ascontiguousarray(p, float), out, g, H)
+        return out[0], g, H.reshape(n, n)
+
+    def discrete(self, z, p, adj=None):
+        """one shooting interval with the stage parameters: x+, A, B (and the adjoint Hessian)"""
+        nx, nu, nz = self.nx, self.nu, self.nz
+        xn, A, B, H = np.zeros(nx), np.zeros(nx * nx), np.zeros(nx * nu), np.zeros(nz * nz)
+        p = np.ascontiguousarray(p, float)
+        a = None if adj is None else np.ascontiguousarray(adj, float)
+        self.L.orc_discrete(C.byref(self.pr), np.ascontiguousarray(z, float), p.ctypes.data_as(C.c_void_p), xn, A, B,
+                            None if a is None else a.ctypes.data_as(C.c_void_p),
+                            None if a is None else H.ctypes.data_as(C.c_void_p))
+        if adj is None:
+            return xn, A.reshape(nx, nx), B.reshape(nx, nu)
+        return xn, A.reshape(nx, nx), B.reshape(nx, nu), H.reshape(nz, nz)
 
     def stage_constraints(self, z, p):
         nh, nz = self.nh, self.nz
@@ -151,22 +191,24 @@ class Oracle:
         return lh, uh
 
     def dynamics(self, z):
-        nx, nz = self.nx, self.nz
-        f, J, H = np.zeros(nx), np.zeros(nx * nz), np.zeros(nx * nz * nz)
+        """continuous model of the integrated states (C3: the 5 bicycle states)"""
+        nxi, nz = (5 if self.layout.model == "bicycle_ca" else self.nx), self.nz
+        f, J, H = np.zeros(nxi), np.zeros(nxi * nz), np.zeros(nxi * nz * nz)
         self.L.orc_dynamics(np.ascontiguousarray(z, float), f, J, H)
-        return f, J.reshape(nx, nz), H.reshape(nx, nz, nz)
+        return f, J.reshape(nxi, nz), H.reshape(nxi, nz, nz)
 
     def erk4(self, z, adj=None):
         nx, nz = self.nx, self.nz
-        xn, A, B = np.zeros(nx), np.zeros(nx * nx), np.zeros(nx * 2)
+        nu = self.nu
+        xn, A, B = np.zeros(nx), np.zeros(nx * nx), np.zeros(nx * nu)
         H = np.zeros(nz * nz)
         if adj is None:
             self.L.orc_erk4(C.byref(self.pr), np.ascontiguousarray(z, float), xn, A, B, None, None)
-            return xn, A.reshape(nx, nx), B.reshape(nx, 2)
+            return xn, A.reshape(nx, nx), B.reshape(nx, nu)
         adj = np.ascontiguousarray(adj, float)
         self.L.orc_erk4(C.byref(self.pr), np.ascontiguousarray(z, float), xn, A, B,
                         adj.ctypes.data_as(C.c_void_p), H.ctypes.data_as(C.c_void_p))
-        return xn, A.reshape(nx, nx), B.reshape(nx, 2), H.reshape(nz, nz)
+        return xn, A.reshape(nx, nx), B.reshape(nx, nu), H.reshape(nz, nz)
 
     def mirror(self, H, eps=1e-4):
         n = H.shape[0]
@@ -176,12 +218,12 @@ class Oracle:
 
     def solve(self, params, warm, xinit):
         N, nx = self.layout.N, self.nx
-        xt, ut = np.zeros((N + 1) * nx), np.zeros(N * 2)
+        xt, ut = np.zeros((N + 1) * nx), np.zeros(N * self.nu)
         info = OrcInfo()
         code = self.L.orc_solve(C.byref(self.pr), np.ascontiguousarray(params, float).ravel(),
                                 np.ascontiguousarray(warm, float).ravel(), np.ascontiguousarray(xinit, float).ravel(),
                                 xt, ut, C.byref(info))
-        return dict(exit=code, xtraj=xt.reshape(N + 1, nx), utraj=ut.reshape(N, 2), pobj=info.pobj,
+        return dict(exit=code, xtraj=xt.reshape(N + 1, nx), utraj=ut.reshape(N, self.nu), pobj=info.pobj,
                     sqp_iter=info.sqp_iter, qp_iter=info.qp_iter_total, qp_status=info.qp_status,
                     res_eq=info.res_eq)
 
@@ -193,7 +235,7 @@ class Oracle:
         N, nx = self.layout.N, self.nx
         B = params.shape[0]
         if lam_in is not None or return_lam:
-            xt, ut = np.zeros((B, N + 1, nx)), np.zeros((B, N, 2))
+            xt, ut = np.zeros((B, N + 1, nx)), np.zeros((B, N, self.nu))
             pobj, st, qi = np.zeros(B), np.zeros(B, np.int32), np.zeros(B, np.int32)
             li = None if lam_in is None else np.ascontiguousarray(lam_in, float).reshape(B, -1)
             lo = np.zeros((B, N, nx + self.layout.nh))
@@ -205,7 +247,7 @@ class Oracle:
                                       lo.ctypes.data_as(C.c_void_p), nthreads)
             return dict(xtraj=xt, utraj=ut, pobj=pobj, status=st, qp_iter=qi, lam=lo)
         xt = np.zeros((B, N + 1, nx))
-        ut = np.zeros((B, N, 2))
+        ut = np.zeros((B, N, self.nu))
         pobj = np.zeros(B)
         st = np.zeros(B, np.int32)
         qi = np.zeros(B, np.int32)

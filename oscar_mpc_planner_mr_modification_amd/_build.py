@@ -16,7 +16,7 @@ ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 # source -> extra flags.  The producers are compiled without floating-point
 # contraction so that they agree bit for bit with the host restatement.
 SOURCES = {"mpcg_kernels.hip": [], "mpcg_prepare.hip": ["-ffp-contract=off"]}
-HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h"]
+HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h", "mpcg_bicycle.h"]
 HOST_SOURCES = ["host/mpcg_yaml.cpp", "host/mpcg_solver.cpp"]
 HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_config.h", "mpc_planner_solver/state.h",
                 "mpc_planner_solver/mpcg_solver_interface.h", "mpc_planner_solver/solver_interface.h"]

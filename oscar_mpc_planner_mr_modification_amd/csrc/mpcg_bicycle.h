@@ -1,0 +1,354 @@
+// mpcg_bicycle.h — C3 stage functions on the device (gfx950, fp64 VALU):
+// BicycleModel2ndOrderCurvatureAware + MPCBase(a, w, slack) +
+// CurvatureAwareContouring; the decomp halfspaces are the kernel's slack rows.
+//
+// Reference semantics (paths relative to the reference repo):
+//   model      solver_model.py:355-396 (bicycle, integrated states x y psi v delta,
+//              beta = atan(l_r / (l_r + l_f) tan delta), l_r = l_f = 2.79 / 2),
+//              :398-437 (the CA spline update s+ = s + R atan2(vt, R - e_c - vn),
+//              R = fmax(1 / curvature, 1e5)); integrated by forces_discrete_dynamics
+//              (:11-36): RK4 over integrator_step (pr.rk_steps steps)
+//   cost       mpc_base.py:47-60 + curvature_aware_contouring.py:48-105, the terminal
+//              terms at stage N-1 as Forces applies them (generate_forces_solver.py:50-59)
+//   spline     spline.py:4-86 (glued value, derivative and second derivative)
+//
+// z = [a, w, slack, x, y, psi, v, delta, s].  Every nonlinear piece depends on
+// at most five stage variables, so derivatives come from second-order jets
+// over five local variables (value, gradient, packed Hessian: 21 doubles);
+// functions of the path coordinate s alone are carried as one-dimensional
+// jets (f, f', f'') and lifted into the stage jets.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcg.h"
+#include "mpcg_device.h"
+
+namespace mpcg {
+namespace bike {
+
+constexpr int NUB = 3, NXB = 6, NZB = NUB + NXB;
+constexpr int ZA = 0, ZW = 1, ZSL = 2, ZX = 3, ZY = 4, ZPSI = 5, ZV = 6, ZDELTA = 7, ZS = 8;
+constexpr double LR = 2.79 / 2.0;          // solver_model.py:383-386
+constexpr double RATIO = LR / (LR + LR);
+constexpr double PI_D = 3.14159265358979323846;
+
+__host__ __device__ constexpr int tri(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+// ---- one-dimensional jets in s: (f, f', f'')
+struct S1 {
+    double v, d, dd;
+};
+__device__ __forceinline__ S1 s1_mul(S1 a, S1 b) { return {a.v * b.v, a.d * b.v + a.v * b.d, a.dd * b.v + 2.0 * a.d * b.d + a.v * b.dd}; }
+__device__ __forceinline__ S1 s1_fn(S1 a, double f, double f1, double f2) { return {f, f1 * a.d, f1 * a.dd + f2 * a.d * a.d}; }
+__device__ __forceinline__ S1 s1_inv(S1 a) { const double i = frcp(a.v); return s1_fn(a, i, -i * i, 2.0 * i * i * i); }
+
+// ---- second-order jets over five local variables
+struct J5 {
+    double v, g[5], h[15];
+};
+__device__ __forceinline__ J5 jconst(double c) {
+    J5 r;
+    r.v = c;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.g[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) r.h[i] = 0.0;
+    return r;
+}
+__device__ __forceinline__ J5 jvar(int i, double x) {
+    J5 r = jconst(x);
+    r.g[i] = 1.0;
+    return r;
+}
+// a one-dimensional s-jet lifted into variable i
+__device__ __forceinline__ J5 jlift(S1 a, int i) {
+    J5 r = jconst(a.v);
+    r.g[i] = a.d;
+    r.h[tri(i, i)] = a.dd;
+    return r;
+}
+// f(a): f' = f1, f'' = f2
+__device__ __forceinline__ J5 jfn(const J5& a, double f, double f1, double f2) {
+    J5 r;
+    r.v = f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.g[i] = f1 * a.g[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) r.h[tri(i, j)] = f1 * a.h[tri(i, j)] + f2 * a.g[i] * a.g[j];
+    return r;
+}
+// f(a, b): partials fa, fb, faa, fab, fbb
+__device__ __forceinline__ J5 jfn2(const J5& a, const J5& b, double f, double fa, double fb, double faa, double fab,
+                                   double fbb) {
+    J5 r;
+    r.v = f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.g[i] = fa * a.g[i] + fb * b.g[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j)
+            r.h[tri(i, j)] = fa * a.h[tri(i, j)] + fb * b.h[tri(i, j)] + faa * a.g[i] * a.g[j] +
+                             fab * (a.g[i] * b.g[j] + b.g[i] * a.g[j]) + fbb * b.g[i] * b.g[j];
+    return r;
+}
+__device__ __forceinline__ J5 operator+(const J5& a, const J5& b) { return jfn2(a, b, a.v + b.v, 1.0, 1.0, 0.0, 0.0, 0.0); }
+__device__ __forceinline__ J5 operator-(const J5& a, const J5& b) { return jfn2(a, b, a.v - b.v, 1.0, -1.0, 0.0, 0.0, 0.0); }
+__device__ __forceinline__ J5 operator*(const J5& a, const J5& b) { return jfn2(a, b, a.v * b.v, b.v, a.v, 0.0, 1.0, 0.0); }
+__device__ __forceinline__ J5 operator*(double c, const J5& a) { return jfn(a, c * a.v, c, 0.0); }
+__device__ __forceinline__ J5 operator+(const J5& a, double c) { return jfn(a, a.v + c, 1.0, 0.0); }
+__device__ __forceinline__ J5 jsq(const J5& a) { return jfn(a, a.v * a.v, 2.0 * a.v, 2.0); }
+__device__ __forceinline__ J5 jinv(const J5& a) { const double i = frcp(a.v); return jfn(a, i, -i * i, 2.0 * i * i * i); }
+__device__ __forceinline__ J5 jcos(const J5& a, double c, double s) { return jfn(a, c, -s, -c); }
+__device__ __forceinline__ J5 jsin(const J5& a, double c, double s) { return jfn(a, s, c, -s); }
+__device__ __forceinline__ J5 jatan2(const J5& y, const J5& x) {
+    const double r2 = x.v * x.v + y.v * y.v, ir2 = frcp(r2), ir4 = ir2 * ir2;
+    return jfn2(y, x, atan2(y.v, x.v), x.v * ir2, -y.v * ir2, -2.0 * x.v * y.v * ir4, (y.v * y.v - x.v * x.v) * ir4,
+                2.0 * x.v * y.v * ir4);
+}
+
+// Glued spline of spline.py:28-58 for one axis: value P, derivative D and
+// second derivative Z, each a jet in s (segment values glued with the sigmoids).
+struct PathJets {
+    S1 P[2], D[2], Z[2];
+};
+__device__ inline void path_jets(const mpcg_problem& pr, const double* __restrict__ p, double s, PathJets& J) {
+    const int M = pr.n_seg;
+    const double* base = p + pr.i_spline0;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        // segment M-1: P, P', P'', P'''
+        const double* c = base + 9 * (M - 1) + 4 * ax;
+        double t = s - base[9 * (M - 1) + 8];
+        double q0 = ((c[0] * t + c[1]) * t + c[2]) * t + c[3], q1 = (3.0 * c[0] * t + 2.0 * c[1]) * t + c[2];
+        double q2 = 6.0 * c[0] * t + 2.0 * c[1], q3 = 6.0 * c[0];
+        S1 P = {q0, q1, q2}, D = {q1, q2, q3}, Z = {q2, q3, 0.0};
+        for (int k = M - 1; k >= 1; --k) {
+            const double e = exp((s - base[9 * k + 8] + 0.02) / 0.1);
+            const double l0 = frcp(1.0 + e);
+            const double l1 = -10.0 * l0 * (1.0 - l0);
+            const double l2 = 100.0 * l0 * (1.0 - l0) * (1.0 - 2.0 * l0);
+            const double m0 = 1.0 - l0;
+            c = base + 9 * (k - 1) + 4 * ax;
+            t = s - base[9 * (k - 1) + 8];
+            q0 = ((c[0] * t + c[1]) * t + c[2]) * t + c[3];
+            q1 = (3.0 * c[0] * t + 2.0 * c[1]) * t + c[2];
+            q2 = 6.0 * c[0] * t + 2.0 * c[1];
+            q3 = 6.0 * c[0];
+            // glue (l * A + (1 - l) * Q) with its first two s-derivatives, A = segment k-1
+            auto glue = [&](S1 Q, double a0, double a1, double a2) -> S1 {
+                return {l0 * a0 + m0 * Q.v, l1 * (a0 - Q.v) + l0 * a1 + m0 * Q.d,
+                        l2 * (a0 - Q.v) + 2.0 * l1 * (a1 - Q.d) + l0 * a2 + m0 * Q.dd};
+            };
+            P = glue(P, q0, q1, q2);
+            D = glue(D, q1, q2, q3);
+            Z = glue(Z, q2, q3, 0.0);
+        }
+        J.P[ax] = P;
+        J.D[ax] = D;
+        J.Z[ax] = Z;
+    }
+}
+
+// unit tangent t = D / |D| (spline.py:72-77) as s-jets
+__device__ __forceinline__ void tangent(const PathJets& J, S1& tx, S1& ty) {
+    const S1 r2 = {J.D[0].v * J.D[0].v + J.D[1].v * J.D[1].v, 2.0 * (J.D[0].v * J.D[0].d + J.D[1].v * J.D[1].d),
+                   2.0 * (J.D[0].d * J.D[0].d + J.D[0].v * J.D[0].dd + J.D[1].d * J.D[1].d + J.D[1].v * J.D[1].dd)};
+    const double ir = frsq(r2.v);  // 1 / sqrt
+    const S1 inr = s1_fn(r2, ir, -0.5 * ir * ir * ir, 0.75 * ir * ir * ir * ir * ir);
+    tx = s1_mul(J.D[0], inr);
+    ty = s1_mul(J.D[1], inr);
+}
+
+// ---------------------------------------------------------------------------
+// stage cost of stage k: MPCBase(a, w, slack) + CA contouring (+ terminal terms
+// at k = N-1).  Jet variables: 0 x, 1 y, 2 psi, 3 v, 4 s.
+// ---------------------------------------------------------------------------
+__device__ inline double stage_cost(const mpcg_problem& pr, const double* __restrict__ p, int k,
+                                    const double z[NZB], double g[NZB], double H[NZB][NZB], bool derivs) {
+    const double wa = p[pr.i_w_acc], ww = p[pr.i_w_ang], ws = p[pr.i_w_slack];
+    const double wc = p[pr.i_w_contour], wv = p[pr.i_w_vel], vref = p[pr.i_v_ref];
+    const double a = z[ZA], w = z[ZW], sl = z[ZSL];
+    PathJets PJ;
+    path_jets(pr, p, z[ZS], PJ);
+    S1 tx1, ty1;
+    tangent(PJ, tx1, ty1);
+    const J5 x = jvar(0, z[ZX]), y = jvar(1, z[ZY]), psi = jvar(2, z[ZPSI]), v = jvar(3, z[ZV]);
+    const J5 tx = jlift(tx1, 4), ty = jlift(ty1, 4);
+    const J5 ex = x - jlift(PJ.P[0], 4), ey = y - jlift(PJ.P[1], 4);
+    // projection_ratio = 1 / (1 - ((x - px) ddx + (y - py) ddy))  (curvature_aware_contouring.py:83-84)
+    const J5 proj = jinv((-1.0) * (ex * jlift(PJ.Z[0], 4) + ey * jlift(PJ.Z[1], 4)) + 1.0);
+    double sp, cp;
+    sincos(z[ZPSI], &sp, &cp);
+    // s_dot = v (cos psi tx + sin psi ty) projection_ratio  (:85)
+    const J5 sdot = (v * (jcos(psi, cp, sp) * tx + jsin(psi, cp, sp) * ty)) * proj;
+    const J5 cerr2 = jsq(ex) + jsq(ey);  // (:88)
+    const J5 verr2 = jsq(sdot + (-vref));
+    J5 L = wc * cerr2 + wv * verr2;      // (:90-91)
+    if (k == pr.N - 1) {                 // terminal terms (:94-103)
+        const double wta = p[pr.i_w_tangle], tc = p[pr.i_w_tcont];
+        const J5 pa = jatan2(ty, tx);
+        // haar_difference_without_abs = fmod(a1 - a2 + pi, 2 pi) - pi (util/math.py:10-11)
+        const J5 d = psi - pa + PI_D;
+        const J5 ae = jfn(d, fmod(d.v, 2.0 * PI_D), 1.0, 0.0) + (-PI_D);
+        L = L + wta * jsq(ae) + (tc * wc) * cerr2 + (tc * wv) * verr2;
+    }
+    const double Lv = wa * a * a + ww * w * w + ws * sl * sl + L.v;
+    if (!derivs) return Lv;
+#pragma unroll
+    for (int i = 0; i < NZB; ++i) {
+        g[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NZB; ++j) H[i][j] = 0.0;
+    }
+    g[ZA] = 2.0 * wa * a; H[ZA][ZA] = 2.0 * wa;
+    g[ZW] = 2.0 * ww * w; H[ZW][ZW] = 2.0 * ww;
+    g[ZSL] = 2.0 * ws * sl; H[ZSL][ZSL] = 2.0 * ws;
+    constexpr int zi[5] = {ZX, ZY, ZPSI, ZV, ZS};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        g[zi[i]] = L.g[i];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) H[zi[i]][zi[j]] = L.h[tri(i, j)];
+    }
+    return Lv;
+}
+
+// ---------------------------------------------------------------------------
+// Discrete map of one shooting interval: RK4 (pr.rk_steps steps over dt) of the
+// five bicycle states, then the CA spline update.  Outputs xn, F = [B A]
+// (nx x nz) and, with pi != nullptr, H += Hess(pi' x+).
+// RK jets over 0 a, 1 w, 2 psi, 3 v, 4 delta; x and y enter the integrated
+// positions additively (x+ = x + dX, y+ = y + dY), so dp = (dX, dY) in the update.
+// ---------------------------------------------------------------------------
+__device__ inline void discrete(const mpcg_problem& pr, const double* __restrict__ p, const double z[NZB],
+                                const double* pi, double xn[NXB], double F[NXB][NZB], double H[NZB][NZB]) {
+    const int ns = pr.rk_steps;
+    const double h = pr.dt / ns;
+    const J5 ja = jvar(0, z[ZA]), jw = jvar(1, z[ZW]);
+    J5 psi = jvar(2, z[ZPSI]), v = jvar(3, z[ZV]), del = jvar(4, z[ZDELTA]);
+    J5 dX = jconst(0.0), dY = jconst(0.0);
+    for (int st = 0; st < ns; ++st) {
+        J5 kx, ky, kp;  // k of the previous RK stage (x, y, psi); v' = a, delta' = w are exact
+        J5 sx = jconst(0.0), sy = jconst(0.0), sp_ = jconst(0.0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double cq = (q == 0) ? 0.0 : ((q == 3) ? 1.0 : 0.5);
+            const double bq = (q == 0 || q == 3) ? 1.0 : 2.0;
+            const J5 pq = q ? psi + (cq * h) * kp : psi;
+            const J5 vq = q ? v + (cq * h) * ja : v;
+            const J5 dq = q ? del + (cq * h) * jw : del;
+            // beta = atan(ratio tan delta)
+            const double td = tan(dq.v);
+            const J5 tq = jfn(dq, td, 1.0 + td * td, 2.0 * td * (1.0 + td * td));
+            const J5 rt = RATIO * tq;
+            const double ib = frcp(1.0 + rt.v * rt.v);
+            const J5 beta = jfn(rt, atan(rt.v), ib, -2.0 * rt.v * ib * ib);
+            const J5 ang = pq + beta;
+            double sa, ca, sb, cb;
+            sincos(ang.v, &sa, &ca);
+            sincos(beta.v, &sb, &cb);
+            kx = vq * jcos(ang, ca, sa);
+            ky = vq * jsin(ang, ca, sa);
+            kp = ((1.0 / LR) * vq) * jsin(beta, cb, sb);
+            sx = sx + bq * kx;
+            sy = sy + bq * ky;
+            sp_ = sp_ + bq * kp;
+        }
+        dX = dX + (h / 6.0) * sx;
+        dY = dY + (h / 6.0) * sy;
+        psi = psi + (h / 6.0) * sp_;
+        v = v + h * ja;
+        del = del + h * jw;
+    }
+    // ---- CA spline update (solver_model.py:409-437); local jets 0 x, 1 y, 2 s, 3 dpx, 4 dpy
+    PathJets PJ;
+    path_jets(pr, p, z[ZS], PJ);
+    S1 tx1, ty1;
+    tangent(PJ, tx1, ty1);
+    const S1 c2 = {PJ.Z[0].v * PJ.Z[0].v + PJ.Z[1].v * PJ.Z[1].v,
+                   2.0 * (PJ.Z[0].v * PJ.Z[0].d + PJ.Z[1].v * PJ.Z[1].d),
+                   2.0 * (PJ.Z[0].d * PJ.Z[0].d + PJ.Z[0].v * PJ.Z[0].dd + PJ.Z[1].d * PJ.Z[1].d + PJ.Z[1].v * PJ.Z[1].dd)};
+    // R = fmax(1 / |Z|, 1e5) = fmax(c2^-1/2, 1e5)
+    const double irc = frsq(c2.v);
+    S1 R1 = s1_fn(c2, irc, -0.5 * irc * irc * irc, 0.75 * irc * irc * irc * irc * irc);
+    if (!(R1.v > 1e5)) R1 = {1e5, 0.0, 0.0};
+    const J5 x = jvar(0, z[ZX]), y = jvar(1, z[ZY]), dpx = jvar(3, dX.v), dpy = jvar(4, dY.v);
+    const J5 tx = jlift(tx1, 2), ty = jlift(ty1, 2), R = jlift(R1, 2);
+    const J5 ec = ty * (x - jlift(PJ.P[0], 2)) - tx * (y - jlift(PJ.P[1], 2));  // (:423)
+    const J5 vt = dpx * tx + dpy * ty;                                         // (:429)
+    const J5 vn = dpx * ty - dpy * tx;                                         // (:430)
+    const J5 G = jvar(2, z[ZS]) + R * jatan2(vt, R - ec - vn);                 // (:435-437)
+
+    xn[0] = z[ZX] + dX.v;
+    xn[1] = z[ZY] + dY.v;
+    xn[2] = psi.v;
+    xn[3] = v.v;
+    xn[4] = del.v;
+    xn[5] = G.v;
+#pragma unroll
+    for (int i = 0; i < NXB; ++i)
+#pragma unroll
+        for (int j = 0; j < NZB; ++j) F[i][j] = 0.0;
+    constexpr int ri[5] = {ZA, ZW, ZPSI, ZV, ZDELTA};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        F[0][ri[j]] = dX.g[j];
+        F[1][ri[j]] = dY.g[j];
+        F[2][ri[j]] = psi.g[j];
+        F[3][ri[j]] = v.g[j];
+        F[4][ri[j]] = del.g[j];
+        F[5][ri[j]] = G.g[3] * dX.g[j] + G.g[4] * dY.g[j];
+    }
+    F[0][ZX] = 1.0;
+    F[1][ZY] = 1.0;
+    F[5][ZX] = G.g[0];
+    F[5][ZY] = G.g[1];
+    F[5][ZS] = G.g[2];
+    if (!pi) return;
+    const double ps = pi[5];
+    const double cX = pi[0] + ps * G.g[3], cY = pi[1] + ps * G.g[4];
+    // (a, w, psi, v, delta) block: second derivatives of the integrated states
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            const double hv = cX * dX.h[tri(i, j)] + cY * dY.h[tri(i, j)] + pi[2] * psi.h[tri(i, j)];
+            H[ri[i]][ri[j]] += hv;
+            if (i != j) H[ri[j]][ri[i]] += hv;
+        }
+    // ps * W' Hess(G) W with W: x -> e_x, y -> e_y, s -> e_s, dpx -> dX.g, dpy -> dY.g
+    double Wm[5][NZB];
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+#pragma unroll
+        for (int j = 0; j < NZB; ++j) Wm[m][j] = 0.0;
+    Wm[0][ZX] = 1.0;
+    Wm[1][ZY] = 1.0;
+    Wm[2][ZS] = 1.0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        Wm[3][ri[j]] = dX.g[j];
+        Wm[4][ri[j]] = dY.g[j];
+    }
+    if (ps != 0.0) {
+#pragma unroll
+        for (int i = 0; i < NZB; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                double acc = 0.0;
+#pragma unroll
+                for (int m = 0; m < 5; ++m)
+#pragma unroll
+                    for (int n = 0; n < 5; ++n) acc += Wm[m][i] * G.h[tri(m, n)] * Wm[n][j];
+                acc *= ps;
+                H[i][j] += acc;
+                if (i != j) H[j][i] += acc;
+            }
+    }
+}
+
+}  // namespace bike
+}  // namespace mpcg

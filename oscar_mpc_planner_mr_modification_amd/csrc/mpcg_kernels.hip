@@ -101,15 +101,18 @@ using Fn = int (*)(const mpcg_problem&, int, const mpcg_io&, hipStream_t);
 
 static Fn find_instance(const mpcg_problem& pr) {
     if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return nullptr;
-#define MPCG_INST(N_, L_, E_, S_, X_)                                                              \
-    if (pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_ && pr.n_scen == S_ && pr.nx == X_) \
-        return &launch<Cfg<N_, L_, E_, S_, X_>>;
-    MPCG_INST(20, 4, 4, 0, 5)    // C1
-    MPCG_INST(20, 8, 8, 0, 5)    // C2 (north star)
-    MPCG_INST(30, 12, 12, 0, 5)  // C4
-    MPCG_INST(20, 0, 0, 24, 6)   // C5 (SH-MPC, slack model)
-    MPCG_INST(10, 2, 2, 0, 5)    // small test instances
-    MPCG_INST(10, 0, 0, 4, 6)
+    if (pr.nu != (pr.model == MPCG_MODEL_BICYCLE_CA ? 3 : 2)) return nullptr;
+#define MPCG_INST(N_, L_, E_, S_, X_, M_)                                                          \
+    if (pr.model == M_ && pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_ && pr.n_scen == S_ && pr.nx == X_) \
+        return &launch<Cfg<N_, L_, E_, S_, X_, M_>>;
+    MPCG_INST(20, 4, 4, 0, 5, 0)    // C1
+    MPCG_INST(20, 8, 8, 0, 5, 0)    // C2 (north star)
+    MPCG_INST(30, 12, 12, 0, 5, 0)  // C4
+    MPCG_INST(20, 0, 0, 24, 6, 0)   // C5 (SH-MPC, slack model)
+    MPCG_INST(30, 0, 0, 12, 6, 1)   // C3 (curvature-aware bicycle + decomp)
+    MPCG_INST(10, 2, 2, 0, 5, 0)    // small test instances
+    MPCG_INST(10, 0, 0, 4, 6, 0)
+    MPCG_INST(10, 0, 0, 4, 6, 1)
 #undef MPCG_INST
     return nullptr;
 }
@@ -118,7 +121,8 @@ static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
     if (!pr || batch < 0) { g_err = "invalid arguments"; return -1; }
     *fn = find_instance(*pr);
     if (!*fn) {
-        g_err = "no compiled instance for N=" + std::to_string(pr->N) + " nx=" + std::to_string(pr->nx) +
+        g_err = "no compiled instance for model=" + std::to_string(pr->model) + " N=" + std::to_string(pr->N) +
+                " nx=" + std::to_string(pr->nx) + " nu=" + std::to_string(pr->nu) +
                 " n_lin=" + std::to_string(pr->n_lin) + " n_ell=" + std::to_string(pr->n_ell) +
                 " n_scen=" + std::to_string(pr->n_scen);
         return -2;
@@ -158,8 +162,16 @@ int mpcg_lam_size(const mpcg_problem* pr) { return pr ? pr->N * (pr->nx + mpcg_n
 
 int mpcg_problem_from_map(mpcg_problem* pr, int N, int nx, int npar, int n_entries, const char* const* names,
                           const int* indices, const double* lb, const double* ub, double dt, int sqp_iters) {
+    return mpcg_problem_from_map_model(pr, MPCG_MODEL_UNICYCLE, N, nx, npar, n_entries, names, indices, lb, ub, dt,
+                                       sqp_iters);
+}
+
+int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int npar, int n_entries,
+                                const char* const* names, const int* indices, const double* lb, const double* ub,
+                                double dt, int sqp_iters) {
+    const bool bike = model == MPCG_MODEL_BICYCLE_CA;
     if (!pr || !names || !indices || !lb || !ub || N < 1 || npar < 1 || n_entries < 0 || nx < 5 ||
-        nx > MPCG_MAX_NX) {
+        nx > MPCG_MAX_NX || (model != MPCG_MODEL_UNICYCLE && !bike) || (bike && nx != 6)) {
         mpcg::g_err = "invalid arguments";
         return -1;
     }
@@ -171,6 +183,8 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int nx, int npar, int n_entri
     std::memset(pr, 0, sizeof(*pr));
     pr->N = N;
     pr->nx = nx;
+    pr->nu = bike ? 3 : MPCG_NU;
+    pr->model = model;
     pr->npar = npar;
     // MPCBase weights (mpc_base.py:47-60), contouring (contouring.py:114-138)
     pr->i_w_acc = find("acceleration");
@@ -189,18 +203,26 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int nx, int npar, int n_entri
     pr->i_disc_off = find("ego_disc_0_offset");
     pr->i_lin0 = find("lin_constraint_0_a1");
     pr->i_ell0 = find("ellipsoid_obst_0_x");
-    // scenario halfspaces (scenario_constraints.py:41-50) and the slack weight
-    pr->i_scen0 = find("disc_0_scenario_constraint_0_a1");
+    // scenario halfspaces (scenario_constraints.py:41-50) or, bicycle, the decomp
+    // halfspaces (decomp_constraints.py:46-54), and the slack weight
+    const std::string rows = bike ? "disc_0_decomp_" : "disc_0_scenario_constraint_";
+    pr->i_scen0 = find(rows + "0_a1");
     pr->i_w_slack = find("slack");
+    pr->i_w_tangle = find("terminal_angle");
+    pr->i_w_tcont = find("terminal_contouring");
     const char* required[] = {"acceleration", "angular_velocity", "velocity", "reference_velocity", "contour",
                               "lag", "spline_x0_a", "ego_disc_0_offset"};
     for (const char* r : required)
         if (find(r) < 0) { mpcg::g_err = std::string("parameter map has no '") + r + "'"; return -1; }
-    if (nx > 5 && pr->i_w_slack < 0) { mpcg::g_err = "parameter map has no 'slack'"; return -1; }
+    if ((nx > 5 || bike) && pr->i_w_slack < 0) { mpcg::g_err = "parameter map has no 'slack'"; return -1; }
+    if (bike && (pr->i_w_tangle < 0 || pr->i_w_tcont < 0)) {
+        mpcg::g_err = "parameter map has no 'terminal_angle' / 'terminal_contouring'";
+        return -1;
+    }
     while (find("spline" + std::to_string(pr->n_seg) + "_start") >= 0) ++pr->n_seg;
     while (find("lin_constraint_" + std::to_string(pr->n_lin) + "_a1") >= 0) ++pr->n_lin;
     while (find("ellipsoid_obst_" + std::to_string(pr->n_ell) + "_x") >= 0) ++pr->n_ell;
-    while (find("disc_0_scenario_constraint_" + std::to_string(pr->n_scen) + "_a1") >= 0) ++pr->n_scen;
+    while (find(rows + std::to_string(pr->n_scen) + "_a1") >= 0) ++pr->n_scen;
     if (pr->n_ell > 0 && pr->i_disc_r < 0) { mpcg::g_err = "parameter map has no 'ego_disc_radius'"; return -1; }
     // the kernels read bundles at fixed strides from their base index: check them
     for (int j = 0; j < pr->n_seg; ++j)
@@ -220,14 +242,17 @@ int mpcg_problem_from_map(mpcg_problem* pr, int N, int nx, int npar, int n_entri
             return -1;
         }
     for (int i = 0; i < pr->n_scen; ++i)
-        if (find("disc_0_scenario_constraint_" + std::to_string(i) + "_b") != pr->i_scen0 + 3 * i + 2) {
+        if (find(rows + std::to_string(i) + "_b") != pr->i_scen0 + 3 * i + 2) {
             mpcg::g_err = "scenario halfspace " + std::to_string(i) + " is not contiguous";
             return -1;
         }
     pr->dt = dt;
-    pr->rk_steps = 3;  // sim_method_num_steps (generate_acados_solver.py:148-150)
-    for (int i = 0; i < MPCG_NU; ++i) { pr->lbu[i] = lb[i]; pr->ubu[i] = ub[i]; }
-    for (int i = 0; i < nx; ++i) { pr->lbx[i] = lb[MPCG_NU + i]; pr->ubx[i] = ub[MPCG_NU + i]; }
+    // sim_method_num_steps (generate_acados_solver.py:148-150); the bicycle: one
+    // Forces RK4 step of integrator_step (solver_model.py:11-36)
+    pr->rk_steps = bike ? 1 : 3;
+    const int nu = pr->nu;
+    for (int i = 0; i < nu; ++i) { pr->lbu[i] = lb[i]; pr->ubu[i] = ub[i]; }
+    for (int i = 0; i < nx; ++i) { pr->lbx[i] = lb[nu + i]; pr->ubx[i] = ub[nu + i]; }
     pr->sqp_iters = sqp_iters;
     pr->qp_tol = 1e-5;
     pr->qp_iter_max = 50;
@@ -267,11 +292,11 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
     const size_t B = max_batch, N = pr->N;
     c->n_par = B * N * pr->npar;
     const size_t nx = pr->nx;
-    c->n_warm = B * (N + 1) * (MPCG_NU + nx);
+    c->n_warm = B * (N + 1) * (pr->nu + nx);
     c->n_xi = B * nx;
     c->n_lam = B * (size_t)mpcg_lam_size(pr);
     c->n_xt = B * (N + 1) * nx;
-    c->n_ut = B * N * MPCG_NU;
+    c->n_ut = B * N * pr->nu;
     c->n_dbl = c->n_par + c->n_warm + c->n_xi + 2 * c->n_lam + c->n_xt + c->n_ut + B;
     c->n_int = B * (1 + MPCG_INFO_STRIDE);
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -316,8 +341,9 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
     const mpcg_problem& pr = c->pr;
     const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr);
     const size_t nx = pr.nx;
-    const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * (MPCG_NU + nx), s_xi = B * nx, s_lam = B * L;
-    const size_t s_xt = B * (N + 1) * nx, s_ut = B * N * MPCG_NU;
+    const size_t nu = pr.nu;
+    const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * (nu + nx), s_xi = B * nx, s_lam = B * L;
+    const size_t s_xt = B * (N + 1) * nx, s_ut = B * N * nu;
     // inputs are packed contiguously (params | warm | xinit | lam_in) so one copy moves them
     double* h = c->host;
     std::memcpy(h, io->params, s_par * sizeof(double));

@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "mpcg.h"
+#include "mpcg_bicycle.h"
 #include "mpcg_device.h"
 
 namespace mpcg {
@@ -40,18 +41,29 @@ __host__ __device__ constexpr int sym(int i, int j) { return i >= j ? i * (i + 1
 __host__ __device__ constexpr int cpk(int n, int a, int c) { return c * n - c * (c - 1) / 2 + (a - c); }
 
 // N: horizon, NL / NE / NS: topology halfspaces, obstacle ellipsoids,
-// scenario halfspaces per stage, NX_: 5 (unicycle) or 6 (unicycle + slack)
-template <int N_, int NL_, int NE_, int NS_ = 0, int NX_ = 5>
+// scenario (or, C3, decomp) halfspaces per stage, NX_: 5 (unicycle) or 6
+// (unicycle + slack state, or the bicycle), MODEL_: 0 contouring unicycle,
+// 1 curvature-aware bicycle (C3: nu 3 with the slack input, mpcg_bicycle.h)
+template <int N_, int NL_, int NE_, int NS_ = 0, int NX_ = 5, int MODEL_ = 0>
 struct Cfg {
-    static constexpr int N = N_, NL = NL_, NE = NE_, NS = NS_;
+    static constexpr int N = N_, NL = NL_, NE = NE_, NS = NS_, MODEL = MODEL_;
+    static constexpr int NU = MODEL_ == 1 ? 3 : 2;
     static constexpr int NX = NX_, NZ = NU + NX_;
-    static_assert(NX == 5 || NX == 6, "unicycle model with or without the slack state");
+    static_assert(MODEL_ == 1 ? NX == 6 : (NX == 5 || NX == 6), "unicycle (+ slack state) or bicycle");
+    // position and heading in z = [u x]; the slack variable (a state of the
+    // SH-MPC unicycle, an input of the bicycle)
+    static constexpr int IX = NU, IY = NU + 1, IPSI = NU + 2;
+    static constexpr bool HAS_SLACK = MODEL_ == 1 || NX > 5;
+    static constexpr int ZSL = MODEL_ == 1 ? 2 : NU + 5;
+    // Cholesky factor of Muu per stage: off-diagonal entries, then reciprocal diagonal
+    static constexpr int NLO = NU * (NU - 1) / 2, NLC = NLO + NU;
+    __host__ __device__ static constexpr int lo_idx(int i, int j) { return i * (i - 1) / 2 + j; }  // i > j
     static constexpr int NH = NL + NE + NS;
     static constexpr int NTRI = NZ * (NZ + 1) / 2;  // packed stage block
     static constexpr int NPT = NX * (NX + 1) / 2;   // packed cost-to-go
     // h rows touch (x, y, psi) and, with the slack model, the slack state:
     // the barrier block of the h rows is NB x NB on those variables
-    static constexpr int NB = (NX > 5 && NS > 0) ? 4 : 3;
+    static constexpr int NB = (HAS_SLACK && NS > 0) ? 4 : 3;
     static constexpr int NBT = NB * (NB + 1) / 2;
     static constexpr int NDH = NZ + NBT + 1;         // dH: diag | block | zero slot
     static constexpr int PARTS = (64 / (N + 1)) >= 3 ? 3 : 2;
@@ -83,10 +95,10 @@ struct Cfg {
     static constexpr int M_TOTAL = 2 * NU + (N - 1) * (NBOX + NH);
     // block index of z variable v (-1: not touched by h rows)
     __host__ __device__ static constexpr int blk(int v) {
-        return (v >= 2 && v <= 4) ? v - 2 : ((NB == 4 && v == NU + 5) ? 3 : -1);
+        return (v >= IX && v <= IPSI) ? v - IX : ((NB == 4 && v == ZSL) ? 3 : -1);
     }
     // z variable of block index b
-    __host__ __device__ static constexpr int bvar(int b) { return b < 3 ? 2 + b : NU + 5; }
+    __host__ __device__ static constexpr int bvar(int b) { return b < 3 ? IX + b : ZSL; }
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -108,8 +120,8 @@ struct Lds {
     double pin[N][NX];
     double rdyn[N][NX];
     double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
-    double Lc[N][4];          // chol(Muu): l00, l10, 1/l00, 1/l11
-    double Y[N][NU][NX];      // L^-1 Mux
+    double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii
+    double Y[N][C::NU][NX];   // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
     double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
     double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
@@ -197,7 +209,7 @@ struct LaneRows {
     // input bounds on every stage < N, state bounds on 1..N-1
     __device__ __forceinline__ bool box_on(int j) const {
         const int v = var(j);
-        return v < C::NZ && (k == 0 ? v < NU : k < C::N);
+        return v < C::NZ && (k == 0 ? v < C::NU : k < C::N);
     }
     __device__ __forceinline__ bool h_on(int r) const { return k >= 1 && k < C::N && hrow(r) < C::NH; }
 };
@@ -208,7 +220,7 @@ template <class C>
 __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __restrict__ pk, const double z[C::NZ],
                                        const LaneRows<C>& LR, const double* nlam, double hb6[6],
                                        double (*Dg)[C::DGC], double* hd, double* disc) {
-    const double x = z[2], y = z[3], psi = z[4];
+    const double x = z[C::IX], y = z[C::IY], psi = z[C::IPSI];
     const double rdisc = C::NE > 0 ? pk[pr.i_disc_r] : 0.0, off = pk[pr.i_disc_off];
     double sp, cp;
     sincos(psi, &sp, &cp);
@@ -234,7 +246,7 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
             // position (scenario_constraints.py:64-94)
             const double* c = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
             if constexpr (!C::LIN_PARAMS) {
-                const double sl = C::NX > 5 ? z[NU + 5] : 0.0;
+                const double sl = C::HAS_SLACK ? z[C::ZSL] : 0.0;
                 hd[hh] = 0.0 - (c[0] * (x + off * cp) + c[1] * (y + off * sp) - (c[2] + sl));
                 Dg[hh][0] = c[0];
                 Dg[hh][1] = c[1];
@@ -278,7 +290,9 @@ template <class C>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
-    constexpr int ZS = NU + 5;  // slack variable (NB == 4)
+    constexpr int NU = C::NU;   // (shadows the unicycle's mpcg::NU)
+    constexpr int ZS = C::ZSL;  // slack variable (NB == 4)
+    constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
     __shared__ Lds<C> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
@@ -337,14 +351,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     };
     auto rowgap = [&](int hh) -> double {
         if constexpr (C::LIN_PARAMS) {
-            const double x = S.z[k][2], y = S.z[k][3];
+            const double x = S.z[k][X0], y = S.z[k][X1];
             if (hh < C::NL) {
                 const double* p = pk + pr.i_lin0 + 3 * hh;
                 return 0.0 - (p[0] * x + p[1] * y - p[2]);
             }
             if (hh >= C::NL + C::NE) {
                 const double* p = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
-                const double sl = C::NX > 5 ? S.z[k][NU + 5] : 0.0;
+                const double sl = C::HAS_SLACK ? S.z[k][ZS] : 0.0;
                 return 0.0 - (p[0] * (x + S.disc[k][0]) + p[1] * (y + S.disc[k][1]) - (p[2] + sl));
             }
             return S.hd[k][hh - C::NL];
@@ -398,11 +412,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             double resl = 0.0;
             if (stage_lane && k < N) {
                 double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
-                stage_cost<NX>(pr, pk, zk, g, H, true);
+                if constexpr (C::MODEL == 1) bike::stage_cost(pr, pk, k, zk, g, H, true);
+                else stage_cost<NX>(pr, pk, zk, g, H, true);
                 STAMP_LAP(11);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
-                erk_unicycle<NX>(pr, zk, pi, xn, F, H);
+                if constexpr (C::MODEL == 1) bike::discrete(pr, pk, zk, pi, xn, F, H);
+                else erk_unicycle<NX>(pr, zk, pi, xn, F, H);
                 STAMP_LAP(12);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -414,12 +430,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 }
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) S.g[k][i] = g[i];
-                H[2][2] += hb6[0]; H[2][3] += hb6[1]; H[3][2] += hb6[1];
-                H[2][4] += hb6[2]; H[4][2] += hb6[2];
-                H[3][3] += hb6[3]; H[3][4] += hb6[4]; H[4][3] += hb6[4];
-                H[4][4] += hb6[5];
+                H[X0][X0] += hb6[0]; H[X0][X1] += hb6[1]; H[X1][X0] += hb6[1];
+                H[X0][X2] += hb6[2]; H[X2][X0] += hb6[2];
+                H[X1][X1] += hb6[3]; H[X1][X2] += hb6[4]; H[X2][X1] += hb6[4];
+                H[X2][X2] += hb6[5];
                 STAMP_LAP(13);
-                if constexpr (NZ == 8) {
+                if constexpr (C::MODEL == 0 && NZ == 8) {
                     // the slack row/column of the slack model is exactly zero off the
                     // diagonal (quadratic slack cost, linear in every h row, no dynamics
                     // coupling): MIRROR of the 8x8 block = MIRROR of the leading 7x7 block
@@ -536,7 +552,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     rowg(hh, a, bq, c);
                     const double l = R.l[HB + r];
                     rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;
-                    double dd = a * dzk[2] + bq * dzk[3] + c * dzk[4];
+                    double dd = a * dzk[X0] + bq * dzk[X1] + c * dzk[X2];
                     if constexpr (NB == 4) {
                         const double sc = C::slack_coef(hh);
                         rh[3] += sc * l;
@@ -738,21 +754,51 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         __syncthreads();
                         STAMP_LAP(17);
                         if (lane < NP) {
-                            const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
-                            // 2x2 Cholesky through reciprocal square roots
-                            const double il00 = frsq(m00);
-                            const double l00 = m00 * il00;
-                            const double l10 = m10 * il00;
-                            const double r11 = m11 - l10 * l10;
-                            const double il11 = frsq(r11);
-                            if (!(m00 > 0.0) || !(r11 > 0.0)) S.flag = 1;
-                            const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
-                            const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
-                            const double y0j = S.Msc[sym(NU + pj_, 0)] * il00;
-                            const double y1j = (S.Msc[sym(NU + pj_, 1)] - l10 * y0j) * il11;
-                            S.P[kk][lane] = S.Msc[sym(NU + pi_, NU + pj_)] - y0i * y0j - y1i * y1j;
-                            if (pj_ == 0) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
-                            if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
+                            // Cholesky of Muu through reciprocal square roots
+                            double Lm[NU][NU], il[NU];
+                            bool bad = false;
+#pragma unroll
+                            for (int j = 0; j < NU; ++j) {
+                                double d = S.Msc[sym(j, j)];
+#pragma unroll
+                                for (int m = 0; m < j; ++m) d -= Lm[j][m] * Lm[j][m];
+                                il[j] = frsq(d);
+                                Lm[j][j] = d * il[j];
+                                bad = bad || !(d > 0.0);
+#pragma unroll
+                                for (int i = j + 1; i < NU; ++i) {
+                                    double acc = S.Msc[sym(i, j)];
+#pragma unroll
+                                    for (int m = 0; m < j; ++m) acc -= Lm[i][m] * Lm[j][m];
+                                    Lm[i][j] = acc * il[j];
+                                }
+                            }
+                            if (bad) S.flag = 1;
+                            double yi[NU], yj[NU];
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) {
+                                double ai = S.Msc[sym(NU + pi_, u)], aj = S.Msc[sym(NU + pj_, u)];
+#pragma unroll
+                                for (int m = 0; m < u; ++m) { ai -= Lm[u][m] * yi[m]; aj -= Lm[u][m] * yj[m]; }
+                                yi[u] = ai * il[u];
+                                yj[u] = aj * il[u];
+                            }
+                            double pv = S.Msc[sym(NU + pi_, NU + pj_)];
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) pv -= yi[u] * yj[u];
+                            S.P[kk][lane] = pv;
+                            if (pj_ == 0) {
+#pragma unroll
+                                for (int u = 0; u < NU; ++u) S.Y[kk][u][pi_] = yi[u];
+                            }
+                            if (lane == 0) {
+#pragma unroll
+                                for (int i = 1; i < NU; ++i)
+#pragma unroll
+                                    for (int j = 0; j < i; ++j) S.Lc[kk][C::lo_idx(i, j)] = Lm[i][j];
+#pragma unroll
+                                for (int u = 0; u < NU; ++u) S.Lc[kk][C::NLO + u] = il[u];
+                            }
                         }
                         STAMP_LAP(18);
                         __syncthreads();
@@ -766,8 +812,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 {
                     const bool own = stage_lane && k < N;
                     const int kq = own ? k : 0;
-                    const double l10 = S.Lc[kq][1], il00 = S.Lc[kq][2], il11 = S.Lc[kq][3];
-                    double G[NX][NX], hv[NX], W0[NX], W1[NX], y0a, y0b;
+                    double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
+#pragma unroll
+                    for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kq][i];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
+                    double G[NX][NX], hv[NX], Wu[NU][NX], y0[NU];
                     {
                         double c[NX], rr[NX];
 #pragma unroll
@@ -787,20 +837,39 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += S.F[kq][j][i] * c[j];
                             m0[i] = a;
                         }
-                        y0a = m0[0] * il00;
-                        y0b = (m0[1] - l10 * y0a) * il11;
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            const double Y0 = S.Y[kq][0][i], Y1 = S.Y[kq][1][i];
-                            hv[i] = m0[NU + i] - Y0 * y0a - Y1 * y0b;
-                            W0[i] = S.F[kq][i][0] * il00;
-                            W1[i] = (S.F[kq][i][1] - l10 * W0[i]) * il11;
+                        for (int u = 0; u < NU; ++u) {
+                            double acc = m0[u];
+#pragma unroll
+                            for (int m = 0; m < u; ++m) acc -= Lo[C::lo_idx(u, m)] * y0[m];
+                            y0[u] = acc * il[u];
                         }
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            const double Y0 = S.Y[kq][0][i], Y1 = S.Y[kq][1][i];
+                            double acc = m0[NU + i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) G[i][j] = S.F[kq][j][NU + i] - Y0 * W0[j] - Y1 * W1[j];
+                            for (int u = 0; u < NU; ++u) acc -= S.Y[kq][u][i] * y0[u];
+                            hv[i] = acc;
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) {
+                                double w = S.F[kq][i][u];
+#pragma unroll
+                                for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wu[m][i];
+                                Wu[u][i] = w * il[u];
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double Yi[NU];
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) Yi[u] = S.Y[kq][u][i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) {
+                                double acc = S.F[kq][j][NU + i];
+#pragma unroll
+                                for (int u = 0; u < NU; ++u) acc -= Yi[u] * Wu[u][j];
+                                G[i][j] = acc;
+                            }
                         }
                     }
                     double pu[NX], pmine[NX];
@@ -824,17 +893,32 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
-                    double ya = y0a, yb = y0b;
+                    double kf[NU];
+                    {
+                        double yy[NU];
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        ya += W0[i] * pmine[i];
-                        yb += W1[i] * pmine[i];
+                        for (int u = 0; u < NU; ++u) {
+                            double acc = y0[u];
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) acc += Wu[u][i] * pmine[i];
+                            yy[u] = acc;
+                        }
+#pragma unroll
+                        for (int u = NU - 1; u >= 0; --u) {
+                            double acc = -yy[u];
+#pragma unroll
+                            for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * kf[m];
+                            kf[u] = acc * il[u];
+                        }
                     }
-                    const double kf1 = -yb * il11;
-                    const double kf0 = (-ya - l10 * kf1) * il00;
                     double e[NX];
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) e[i] = S.rdyn[kq][i] + S.F[kq][i][0] * kf0 + S.F[kq][i][1] * kf1;
+                    for (int i = 0; i < NX; ++i) {
+                        double acc = S.rdyn[kq][i];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) acc += S.F[kq][i][u] * kf[u];
+                        e[i] = acc;
+                    }
                     double dxu[NX], dxmine[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) { dxu[i] = 0.0; dxmine[i] = 0.0; }
@@ -856,13 +940,21 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     if (own) {
-                        double du1 = kf1, du0 = kf0, dxn[NX];
+                        double du[NU], dxn[NX];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) du[u] = kf[u];
 #pragma unroll
                         for (int j = 0; j < NX; ++j) {
-                            const double K1 = -S.Y[k][1][j] * il11;
-                            const double K0 = (-S.Y[k][0][j] - l10 * K1) * il00;
-                            du0 += K0 * dxmine[j];
-                            du1 += K1 * dxmine[j];
+                            double K[NU];
+#pragma unroll
+                            for (int u = NU - 1; u >= 0; --u) {
+                                double acc = -S.Y[k][u][j];
+#pragma unroll
+                                for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * K[m];
+                                K[u] = acc * il[u];
+                            }
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) du[u] += K[u] * dxmine[j];
                         }
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
@@ -871,8 +963,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += G[j][i] * dxmine[j];
                             dxn[i] = a;
                         }
-                        S.ddz[k][0] = du0;
-                        S.ddz[k][1] = du1;
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) S.ddz[k][u] = du[u];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             S.ddz[k][NU + i] = (k == 0) ? 0.0 : dxmine[i];
@@ -882,8 +974,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
-                            S.ddz[N][0] = 0.0;
-                            S.ddz[N][1] = 0.0;
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) S.ddz[N][u] = 0.0;
 #pragma unroll
                             for (int i = 0; i < NX; ++i) S.ddz[N][NU + i] = dxn[i];
                         }
@@ -912,7 +1004,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             const int hh = LR.hrow(r);
                             double ga, gb, gc;
                             rowg(hh, ga, gb, gc);
-                            v = ga * ddk[2] + gb * ddk[3] + gc * ddk[4];
+                            v = ga * ddk[X0] + gb * ddk[X1] + gc * ddk[X2];
                             if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
                         }
                         ddh[r] = v;
@@ -1004,7 +1096,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         if (stage_lane) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) S.z[k][i] += S.dz[k][i];
-            if (k == N) { S.z[N][0] = 0.0; S.z[N][1] = 0.0; }
+            if (k == N) {
+#pragma unroll
+                for (int u = 0; u < NU; ++u) S.z[N][u] = 0.0;
+            }
             if (k < N) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) S.pi_nlp[k][i] = S.piq[k][i];
@@ -1024,7 +1119,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         double zz[NZ], gd[NZ], Hd[NZ][NZ];
 #pragma unroll
         for (int i = 0; i < NZ; ++i) zz[i] = S.z[k][i];
-        Lk = stage_cost<NX>(pr, pk, zz, gd, Hd, false);
+        if constexpr (C::MODEL == 1) Lk = bike::stage_cost(pr, pk, k, zz, gd, Hd, false);
+        else Lk = stage_cost<NX>(pr, pk, zz, gd, Hd, false);
     }
     const double pobj = wave_sum(Lk);
     double* xo = io.xtraj + (size_t)sol * (N + 1) * NX;

@@ -26,6 +26,11 @@ UNICYCLE_INPUTS = ("a", "w")
 SLACK_LB = UNICYCLE_LB + (0.0,)
 SLACK_UB = UNICYCLE_UB + (5000.0,)
 SLACK_STATES = UNICYCLE_STATES + ("slack",)
+# BicycleModel2ndOrderCurvatureAware (solver_model.py:355-376), z = [a, w, slack, x, y, psi, v, delta, s]
+BICYCLE_LB = (-3.0, -1.5, 0.0, -1.0e6, -1.0e6, -12.566370614359172, -0.01, -0.55, -1.0)
+BICYCLE_UB = (3.0, 1.5, 1.0e2, 1.0e6, 1.0e6, 12.566370614359172, 8.0, 0.55, 5000.0)
+BICYCLE_STATES = ("x", "y", "psi", "v", "delta", "spline")
+BICYCLE_INPUTS = ("a", "w", "slack")
 
 
 class _Params:
@@ -90,6 +95,16 @@ def _scenario(p: _Params, n_discs: int, n_constraints: int):
                 p.add(f"disc_{d}_scenario_constraint_{i}_{c}")
 
 
+def _decomp(p: _Params, n_discs: int, max_constraints: int):
+    # decomp_constraints.py:46-54
+    for d in range(n_discs):
+        p.add(f"ego_disc_{d}_offset", "ego_disc_offset")
+        for i in range(max_constraints):
+            p.add(f"disc_{d}_decomp_{i}_a1", "decomp_a1")
+            p.add(f"disc_{d}_decomp_{i}_a2", "decomp_a2")
+            p.add(f"disc_{d}_decomp_{i}_b", "decomp_b")
+
+
 def _ellipsoid(p: _Params, n_discs: int, n_obs: int):
     # ellipsoid_constraints.py:406-419
     p.add("ego_disc_radius")
@@ -110,7 +125,7 @@ class Layout:
     n_ell: int
     n_seg: int = 5
     consistency: bool = True
-    model: str = "unicycle"      # or "unicycle_slack" (slack state last)
+    model: str = "unicycle"      # "unicycle_slack" (slack state last) or "bicycle_ca" (C3)
     n_scen: int = 0
     dt: float = 0.2
     rk_steps: int = 3
@@ -124,11 +139,16 @@ class Layout:
 
     @property
     def nx(self) -> int:
-        return 6 if self.model == "unicycle_slack" else 5
+        return 5 if self.model == "unicycle" else 6
 
     @property
     def nu(self) -> int:
-        return 2
+        return 3 if self.model == "bicycle_ca" else 2
+
+    @property
+    def model_id(self) -> int:
+        """mpcg_problem.model (include/mpcg.h): 0 contouring unicycle, 1 curvature-aware bicycle"""
+        return 1 if self.model == "bicycle_ca" else 0
 
     @property
     def nvar(self) -> int:
@@ -140,15 +160,19 @@ class Layout:
 
     @property
     def states(self):
-        return SLACK_STATES if self.model == "unicycle_slack" else UNICYCLE_STATES
+        return {"unicycle_slack": SLACK_STATES, "bicycle_ca": BICYCLE_STATES}.get(self.model, UNICYCLE_STATES)
+
+    @property
+    def inputs(self):
+        return BICYCLE_INPUTS if self.model == "bicycle_ca" else UNICYCLE_INPUTS
 
     @property
     def lb(self):
-        return SLACK_LB if self.model == "unicycle_slack" else UNICYCLE_LB
+        return {"unicycle_slack": SLACK_LB, "bicycle_ca": BICYCLE_LB}.get(self.model, UNICYCLE_LB)
 
     @property
     def ub(self):
-        return SLACK_UB if self.model == "unicycle_slack" else UNICYCLE_UB
+        return {"unicycle_slack": SLACK_UB, "bicycle_ca": BICYCLE_UB}.get(self.model, UNICYCLE_UB)
 
     def idx(self, name: str) -> int:
         return self.pmap.get(name, -1)
@@ -164,8 +188,10 @@ class Layout:
             i_lin0=g("lin_constraint_0_a1") if self.n_lin else -1,
             i_disc_r=g("ego_disc_radius"), i_disc_off=g("ego_disc_0_offset"),
             i_ell0=g("ellipsoid_obst_0_x") if self.n_ell else -1,
-            i_scen0=g("disc_0_scenario_constraint_0_a1") if self.n_scen else -1,
+            i_scen0=(g("disc_0_decomp_0_a1") if self.model == "bicycle_ca" else
+                     g("disc_0_scenario_constraint_0_a1")) if self.n_scen else -1,
             i_w_slack=g("slack"),
+            i_w_tangle=g("terminal_angle"), i_w_tcont=g("terminal_contouring"),
         )
 
 
@@ -207,7 +233,23 @@ def safe_horizon_layout(N: int = 20, n_constraints: int = 24, num_segments: int 
                   pmap=p.map, bundles=p.bundles)
 
 
-# BASELINE.json configs on the unicycle T-MPC problem
+def ca_decomp_layout(N: int = 30, max_constraints: int = 12, num_segments: int = 5) -> Layout:
+    """C3: BicycleModel2ndOrderCurvatureAware + MPCBase(a, w, slack) +
+    CurvatureAwareContouring (curvature_aware_contouring.py:22-44, same parameter order as
+    contouring) + DecompConstraints(max_constraints, decomp_constraints.py:46-54).  The
+    decomp halfspaces are the slack rows of the kernel (n_scen).  The reference discretises
+    this model with Forces only (solver_model.py:11-36): one RK4 step of integrator_step."""
+    p = _Params()
+    for n in ("acceleration", "angular_velocity", "slack"):
+        p.add(n)
+    _contouring(p, num_segments)
+    _decomp(p, 1, max_constraints)
+    return Layout(name=f"cadecomp_N{N}_dec{max_constraints}", N=N, max_obstacles=0, n_lin=0, n_ell=0,
+                  n_seg=num_segments, consistency=False, model="bicycle_ca", n_scen=max_constraints,
+                  rk_steps=1, pmap=p.map, bundles=p.bundles)
+
+
+# BASELINE.json configs
 def config_layout(cfg: str) -> Layout:
     cfg = cfg.upper()
     if cfg == "C1":
@@ -220,4 +262,8 @@ def config_layout(cfg: str) -> Layout:
         lay = safe_horizon_layout(N=20, n_constraints=24)
         lay.name = "C5"
         return lay
-    raise KeyError(f"config {cfg} has no layout (C3, the bicycle CA-MPC problem, is not built)")
+    if cfg == "C3":
+        lay = ca_decomp_layout(N=30, max_constraints=12)
+        lay.name = "C3"
+        return lay
+    raise KeyError(f"config {cfg} has no layout")

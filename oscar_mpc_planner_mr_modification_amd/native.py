@@ -40,6 +40,9 @@ def _load():
     lib.mpcg_problem_from_map.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_char_p),
                                           C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.c_double, C.c_int]
+    lib.mpcg_problem_from_map_model.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.POINTER(C.c_char_p), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                                C.POINTER(C.c_double), C.c_double, C.c_int]
     lib.mpcg_solve.argtypes = [P, C.c_int, C.POINTER(MpcgIo), vp]
     lib.mpcg_solve.restype = C.c_int
     lib.mpcg_context_create.argtypes = [P, C.c_int]
@@ -98,7 +101,7 @@ def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=No
     import torch
 
     B = params.shape[0]
-    N, nx = pr.N, pr.nx
+    N, nx, NU = pr.N, pr.nx, pr.nu
     LS = lam_stride(pr)
     assert params.dtype == torch.float64 and params.is_cuda and params.is_contiguous()
     assert tuple(params.shape) == (B, N, pr.npar), (tuple(params.shape), (B, N, pr.npar))
@@ -153,7 +156,7 @@ class Context:
 
     def solve(self, params, warm, xinit, lam_in=None, lam_out=False):
         pr = self.pr
-        B, N, nx = params.shape[0], pr.N, pr.nx
+        B, N, nx, NU = params.shape[0], pr.N, pr.nx, pr.nu
         LS = lam_stride(pr)
         params = np.ascontiguousarray(params, np.float64)
         warm = np.ascontiguousarray(warm, np.float64)
@@ -176,7 +179,7 @@ class Context:
 def solve_batch_host(pr: MpcgProblem, params: np.ndarray, warm: np.ndarray, xinit: np.ndarray):
     """Host-buffer solve through the same kernels (copies in/out, synchronous)."""
     B = params.shape[0]
-    N, nx = pr.N, pr.nx
+    N, nx, NU = pr.N, pr.nx, pr.nu
     params = np.ascontiguousarray(params, np.float64)
     warm = np.ascontiguousarray(warm, np.float64)
     xinit = np.ascontiguousarray(xinit, np.float64)

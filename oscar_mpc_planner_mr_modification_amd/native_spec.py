@@ -10,8 +10,8 @@ import numpy as np
 
 from .layouts import Layout
 
-NX, NU, NVAR = 5, 2, 7   # the T-MPC unicycle; the SH-MPC slack model has nx 6 (Layout.nx)
-MAX_NX = 6
+NX, NU, NVAR = 5, 2, 7   # the T-MPC unicycle; the SH-MPC slack model has nx 6, the C3 bicycle nu 3 / nx 6
+MAX_NX, MAX_NU = 6, 3
 INFO_STRIDE = 4
 
 
@@ -29,11 +29,12 @@ class MpcgProblem(C.Structure):
         ("i_ell0", C.c_int),
         ("n_scen", C.c_int), ("i_scen0", C.c_int), ("i_w_slack", C.c_int), ("nx", C.c_int),
         ("dt", C.c_double), ("rk_steps", C.c_int),
-        ("lbu", C.c_double * 2), ("ubu", C.c_double * 2),
+        ("lbu", C.c_double * MAX_NU), ("ubu", C.c_double * MAX_NU),
         ("lbx", C.c_double * MAX_NX), ("ubx", C.c_double * MAX_NX),
         ("sqp_iters", C.c_int), ("qp_tol", C.c_double), ("qp_iter_max", C.c_int),
         ("reg_eps", C.c_double), ("qp_mu0", C.c_double), ("qp_thr0", C.c_double),
         ("res_eq_fail", C.c_double),
+        ("nu", C.c_int), ("model", C.c_int), ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int),
     ]
 
 
@@ -52,15 +53,17 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.n_lin, pr.n_ell, pr.n_seg = layout.n_lin, layout.n_ell, layout.n_seg
     pr.n_scen = layout.n_scen
     pr.nx = nx = layout.nx
+    pr.nu = nu = layout.nu
+    pr.model = layout.model_id
     for k, v in layout.index_struct().items():
         setattr(pr, k, v)
     pr.dt = o.get("dt", layout.dt)
     pr.rk_steps = o.get("rk_steps", layout.rk_steps)
     lb, ub = o.get("lb", layout.lb), o.get("ub", layout.ub)
-    for i in range(NU):
+    for i in range(nu):
         pr.lbu[i], pr.ubu[i] = lb[i], ub[i]
     for i in range(nx):
-        pr.lbx[i], pr.ubx[i] = lb[NU + i], ub[NU + i]
+        pr.lbx[i], pr.ubx[i] = lb[nu + i], ub[nu + i]
     pr.sqp_iters = o.get("sqp_iters", layout.sqp_iters)
     pr.qp_tol = o["qp_tol"]
     pr.qp_iter_max = o["qp_iter_max"]
@@ -103,9 +106,9 @@ class MpcgScenarioIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
-           "mpcg_problem_from_map", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
+           "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
            "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device")
 

@@ -77,5 +77,14 @@ def fmax(a, b):
     return _sp.Max(a, b)
 
 
-def fmod(a, b):
-    return _sp.Mod(a, b)
+class fmod(_sp.Function):
+    """C fmod (casadi's fmod), left unevaluated: sympy's Mod would try to
+    simplify the symbolic dividend (slow) and takes the floor convention.
+    d/da = 1; lambdify it with {"fmod": numpy.fmod}."""
+
+    def fdiff(self, argindex=1):
+        a, b = self.args
+        if argindex == 1:
+            return _sp.S.One
+        q = a / b
+        return -_sp.sign(q) * _sp.floor(_sp.Abs(q))

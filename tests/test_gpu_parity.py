@@ -97,6 +97,27 @@ def test_parity_shmpc_slack_model(native, torch_dev, oracle_mod, N, n_scen, n_sc
                           select_lowest_cost(ref["pobj"], ref["status"], b.n_solvers))
 
 
+@pytest.mark.parametrize("N,n_dec,n_scenes,seed", [(30, 12, 48, 20251212), (10, 4, 16, 9)])
+def test_parity_c3_bicycle(native, torch_dev, oracle_mod, N, n_dec, n_scenes, seed):
+    """C3: curvature-aware bicycle (nu 3 with the slack input, nx 6, one RK4 step
+    + the CA spline update), CurvatureAwareContouring with the terminal terms at
+    stage N-1, decomp halfspaces with slack."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch
+    from oscar_mpc_planner_mr_modification_amd.layouts import ca_decomp_layout, config_layout
+
+    lay = config_layout("C3") if (N, n_dec) == (30, 12) else ca_decomp_layout(N=N, max_constraints=n_dec)
+    b = make_c3_batch(lay, n_scenes, seed=seed)
+    ref = oracle_mod.Oracle(lay).solve_batch(b.params, b.warm, b.xinit)
+    pr = native.problem_from_layout(lay)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(torch_dev)  # noqa: E731
+    out = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit))
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    assert got["xtraj"].shape == (n_scenes, N + 1, 6) and got["utraj"].shape == (n_scenes, N, 3)
+    _compare(ref, got, f"C3 N={N} decomp={n_dec}")
+
+
 def test_single_rti_iteration(native, torch_dev, oracle_mod):
     """one SQP-RTI iteration == solver_type SQP path (acados_solver_interface.cpp:28-29)"""
     lay, b, ref, got = _run(native, torch_dev, oracle_mod, "C2", 4, 8, 99, sqp_iters=1)
