@@ -56,7 +56,8 @@ struct Cfg {
     static constexpr bool HAS_SLACK = MODEL_ == 1 || NX > 5;
     static constexpr int ZSL = MODEL_ == 1 ? 2 : NU + 5;
     // Cholesky factor of Muu per stage: off-diagonal entries, then reciprocal diagonal
-    static constexpr int NLO = NU * (NU - 1) / 2, NLC = NLO + NU;
+    // (nu 2: l00, l10, 1/l00, 1/l11, the layout of the unicycle's hand-unrolled code)
+    static constexpr int NLO = NU * (NU - 1) / 2, NLC = NU == 2 ? 4 : NLO + NU;
     __host__ __device__ static constexpr int lo_idx(int i, int j) { return i * (i - 1) / 2 + j; }  // i > j
     static constexpr int NH = NL + NE + NS;
     static constexpr int NTRI = NZ * (NZ + 1) / 2;  // packed stage block
@@ -120,7 +121,7 @@ struct Lds {
     double pin[N][NX];
     double rdyn[N][NX];
     double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
-    double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii
+    double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
     double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
@@ -753,7 +754,25 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         STAMP_LAP(16);
                         __syncthreads();
                         STAMP_LAP(17);
-                        if (lane < NP) {
+                        if constexpr (NU == 2) {
+                          if (lane < NP) {
+                            const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
+                            // 2x2 Cholesky through reciprocal square roots
+                            const double il00 = frsq(m00);
+                            const double l00 = m00 * il00;
+                            const double l10 = m10 * il00;
+                            const double r11 = m11 - l10 * l10;
+                            const double il11 = frsq(r11);
+                            if (!(m00 > 0.0) || !(r11 > 0.0)) S.flag = 1;
+                            const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
+                            const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
+                            const double y0j = S.Msc[sym(NU + pj_, 0)] * il00;
+                            const double y1j = (S.Msc[sym(NU + pj_, 1)] - l10 * y0j) * il11;
+                            S.P[kk][lane] = S.Msc[sym(NU + pi_, NU + pj_)] - y0i * y0j - y1i * y1j;
+                            if (pj_ == 0) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
+                            if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
+                          }
+                        } else if (lane < NP) {
                             // Cholesky of Muu through reciprocal square roots
                             double Lm[NU][NU], il[NU];
                             bool bad = false;
@@ -813,10 +832,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     const bool own = stage_lane && k < N;
                     const int kq = own ? k : 0;
                     double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
+                    if constexpr (NU == 2) {
+                        Lo[0] = S.Lc[kq][1]; il[0] = S.Lc[kq][2]; il[1] = S.Lc[kq][3];
+                    } else {
 #pragma unroll
-                    for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kq][i];
+                        for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kq][i];
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
+                        for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
+                    }
                     double G[NX][NX], hv[NX], Wu[NU][NX], y0[NU];
                     {
                         double c[NX], rr[NX];
