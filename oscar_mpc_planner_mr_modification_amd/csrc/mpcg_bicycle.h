@@ -227,42 +227,43 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
                                 const double* pi, double xn[NXB], double F[NXB][NZB], double H[NZB][NZB]) {
     const int ns = pr.rk_steps;
     const double h = pr.dt / ns;
-    const J5 ja = jvar(0, z[ZA]), jw = jvar(1, z[ZW]);
-    J5 psi = jvar(2, z[ZPSI]), v = jvar(3, z[ZV]), del = jvar(4, z[ZDELTA]);
-    J5 dX = jconst(0.0), dY = jconst(0.0);
+    // v' = a and delta' = w are integrated exactly (v_q = v + tau a, delta_q = delta + tau w at
+    // every RK stage argument), so their jets stay sparse; psi, dX, dY carry the nonlinearity.
+    J5 psi = jvar(2, z[ZPSI]), dX = jconst(0.0), dY = jconst(0.0);
     for (int st = 0; st < ns; ++st) {
-        J5 kx, ky, kp;  // k of the previous RK stage (x, y, psi); v' = a, delta' = w are exact
-        J5 sx = jconst(0.0), sy = jconst(0.0), sp_ = jconst(0.0);
+        J5 kp, sx = jconst(0.0), sy = jconst(0.0), sp_ = jconst(0.0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const double cq = (q == 0) ? 0.0 : ((q == 3) ? 1.0 : 0.5);
             const double bq = (q == 0 || q == 3) ? 1.0 : 2.0;
+            const double tau = (st + cq) * h;
             const J5 pq = q ? psi + (cq * h) * kp : psi;
-            const J5 vq = q ? v + (cq * h) * ja : v;
-            const J5 dq = q ? del + (cq * h) * jw : del;
+            J5 vq = jvar(3, z[ZV] + tau * z[ZA]);
+            vq.g[0] = tau;
+            J5 dq = jvar(4, z[ZDELTA] + tau * z[ZW]);
+            dq.g[1] = tau;
             // beta = atan(ratio tan delta)
             const double td = tan(dq.v);
-            const J5 tq = jfn(dq, td, 1.0 + td * td, 2.0 * td * (1.0 + td * td));
-            const J5 rt = RATIO * tq;
-            const double ib = frcp(1.0 + rt.v * rt.v);
-            const J5 beta = jfn(rt, atan(rt.v), ib, -2.0 * rt.v * ib * ib);
+            const double rt = RATIO * td, ib = frcp(1.0 + rt * rt);
+            // d beta / d delta and d2 beta / d delta2 through rt = ratio tan(delta)
+            const double rt1 = RATIO * (1.0 + td * td), rt2 = RATIO * 2.0 * td * (1.0 + td * td);
+            const J5 beta = jfn(dq, atan(rt), ib * rt1, ib * rt2 - 2.0 * rt * ib * ib * rt1 * rt1);
             const J5 ang = pq + beta;
             double sa, ca, sb, cb;
             sincos(ang.v, &sa, &ca);
             sincos(beta.v, &sb, &cb);
-            kx = vq * jcos(ang, ca, sa);
-            ky = vq * jsin(ang, ca, sa);
+            sx = sx + bq * (vq * jcos(ang, ca, sa));
+            sy = sy + bq * (vq * jsin(ang, ca, sa));
             kp = ((1.0 / LR) * vq) * jsin(beta, cb, sb);
-            sx = sx + bq * kx;
-            sy = sy + bq * ky;
             sp_ = sp_ + bq * kp;
         }
         dX = dX + (h / 6.0) * sx;
         dY = dY + (h / 6.0) * sy;
         psi = psi + (h / 6.0) * sp_;
-        v = v + h * ja;
-        del = del + h * jw;
     }
+    J5 v = jvar(3, z[ZV] + pr.dt * z[ZA]), del = jvar(4, z[ZDELTA] + pr.dt * z[ZW]);
+    v.g[0] = pr.dt;
+    del.g[1] = pr.dt;
     // ---- CA spline update (solver_model.py:409-437); local jets 0 x, 1 y, 2 s, 3 dpx, 4 dpy
     PathJets PJ;
     path_jets(pr, p, z[ZS], PJ);

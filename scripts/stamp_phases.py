@@ -20,7 +20,11 @@ NS = len(PH)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 scenes = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 lay = config_layout(cfg)
-b = make_batch(lay, scenes, 8, workers=16)
+if cfg == "C3":
+    from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch  # noqa: E402
+    b = make_c3_batch(lay, scenes)
+else:
+    b = make_batch(lay, scenes, 8, workers=16)
 dev = torch.device("cuda:0")
 t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
 B = b.params.shape[0]
