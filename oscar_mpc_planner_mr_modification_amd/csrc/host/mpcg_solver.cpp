@@ -157,8 +157,9 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
     if (N != SOLVER_N || (int)npar != SOLVER_NP || (int)nx != SOLVER_NX || (int)nu != SOLVER_NU)
         fatal("solver_settings.yaml (N=" + std::to_string(N) + ", npar=" + std::to_string(npar) +
               ") does not match the compiled dimensions in mpcg_solver_dims.h");
-    if ((nx != 5 && nx != 6) || nu != MPCG_NU)
-        fatal("the MI355X backend implements the contouring unicycle model (nx 5, or 6 with the slack state)");
+    if (SOLVER_MODEL == MPCG_MODEL_BICYCLE_CA ? (nx != 6 || nu != 3) : ((nx != 5 && nx != 6) || nu != MPCG_NU))
+        fatal("the MI355X backend implements the contouring unicycle model (nx 5, or 6 with the slack state) and "
+              "the curvature-aware bicycle (nx 6, nu 3)");
 
     const mpcg::YamlNode& cfg = SolverConfig::settings();
     dt = cfg["integrator_step"].as<double>();
@@ -183,8 +184,8 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
         lb[i] = it->second[2].as<double>();
         ub[i] = it->second[3].as<double>();
     }
-    if (mpcg_problem_from_map(&_problem, N, (int)nx, npar, (int)names.size(), cnames.data(), idx.data(), lb.data(), ub.data(),
-                              dt, _num_iterations) != 0)
+    if (mpcg_problem_from_map_model(&_problem, SOLVER_MODEL, N, (int)nx, npar, (int)names.size(), cnames.data(),
+                                    idx.data(), lb.data(), ub.data(), dt, _num_iterations) != 0)
         fatal(std::string("parameter map: ") + mpcg_last_error());
     if (mpcg_supported(&_problem) != 0)
         fatal("no compiled kernel instance for N=" + std::to_string(N) + ", nx=" + std::to_string(nx) + " with " +

@@ -101,7 +101,13 @@ static void test_plumbing() {
     setSolverParameterLinConstraintB(6, solver._params, -1.25, 3);
     CHECK(solver.getParameter(6, "lin_constraint_3_b") == -1.25);
 #endif
-#if SOLVER_N_SCEN > 3
+#if SOLVER_MODEL == 1 && SOLVER_N_SCEN > 3
+    // decomp_constraints.py:46-54: bundles decomp_a1 / decomp_a2 / decomp_b over the constraint index
+    setSolverParameterDecompB(6, solver._params, -1.25, 3);
+    CHECK(solver.getParameter(6, "disc_0_decomp_3_b") == -1.25);
+    setSolverParameterSlack(1, solver._params, 10000.);
+    CHECK(solver.getParameter(1, "slack") == 10000.);
+#elif SOLVER_N_SCEN > 3
     // scenario_constraints.py:41-50: one bundle per scalar
     setSolverParameterDisc0ScenarioConstraint3B(6, solver._params, -1.25);
     CHECK(solver.getParameter(6, "disc_0_scenario_constraint_3_b") == -1.25);
