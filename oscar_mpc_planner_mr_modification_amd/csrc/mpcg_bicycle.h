@@ -219,23 +219,27 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
 // ---------------------------------------------------------------------------
 // Discrete map of one shooting interval: RK4 (pr.rk_steps steps over dt) of the
 // five bicycle states, then the CA spline update.  Outputs xn, F = [B A]
-// (nx x nz) and, with pi != nullptr, H += Hess(pi' x+).
+// (nx x nz, written straight to `F`, LDS in the kernel) and Hp = Hess(pi' x+)
+// packed (lower triangle over z, sym index).
 // RK jets over 0 a, 1 w, 2 psi, 3 v, 4 delta; x and y enter the integrated
 // positions additively (x+ = x + dX, y+ = y + dY), so dp = (dX, dY) in the update.
+// Written to keep few jets live at once (the linearisation lane's registers):
+// F rows and the psi Hessian leave before the update is evaluated.
 // ---------------------------------------------------------------------------
 __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict__ p, const double z[NZB],
-                                const double* pi, double xn[NXB], double F[NXB][NZB], double H[NZB][NZB]) {
+                                const double* pi, double xn[NXB], double (*F)[NZB], double Hp[NZB * (NZB + 1) / 2]) {
     const int ns = pr.rk_steps;
     const double h = pr.dt / ns;
     // v' = a and delta' = w are integrated exactly (v_q = v + tau a, delta_q = delta + tau w at
     // every RK stage argument), so their jets stay sparse; psi, dX, dY carry the nonlinearity.
     J5 psi = jvar(2, z[ZPSI]), dX = jconst(0.0), dY = jconst(0.0);
     for (int st = 0; st < ns; ++st) {
-        J5 kp, sx = jconst(0.0), sy = jconst(0.0), sp_ = jconst(0.0);
+        // the step's increments go straight into dX, dY and the psi accumulator
+        J5 kp, psin = psi;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const double cq = (q == 0) ? 0.0 : ((q == 3) ? 1.0 : 0.5);
-            const double bq = (q == 0 || q == 3) ? 1.0 : 2.0;
+            const double wq = ((q == 0 || q == 3) ? 1.0 : 2.0) * h / 6.0;
             const double tau = (st + cq) * h;
             const J5 pq = q ? psi + (cq * h) * kp : psi;
             J5 vq = jvar(3, z[ZV] + tau * z[ZA]);
@@ -252,18 +256,42 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
             double sa, ca, sb, cb;
             sincos(ang.v, &sa, &ca);
             sincos(beta.v, &sb, &cb);
-            sx = sx + bq * (vq * jcos(ang, ca, sa));
-            sy = sy + bq * (vq * jsin(ang, ca, sa));
+            dX = dX + wq * (vq * jcos(ang, ca, sa));
+            dY = dY + wq * (vq * jsin(ang, ca, sa));
             kp = ((1.0 / LR) * vq) * jsin(beta, cb, sb);
-            sp_ = sp_ + bq * kp;
+            psin = psin + wq * kp;
         }
-        dX = dX + (h / 6.0) * sx;
-        dY = dY + (h / 6.0) * sy;
-        psi = psi + (h / 6.0) * sp_;
+        psi = psin;
     }
-    J5 v = jvar(3, z[ZV] + pr.dt * z[ZA]), del = jvar(4, z[ZDELTA] + pr.dt * z[ZW]);
-    v.g[0] = pr.dt;
-    del.g[1] = pr.dt;
+    constexpr int ri[5] = {ZA, ZW, ZPSI, ZV, ZDELTA};
+    // rows x+, y+, psi+, v+ = v + dt a, delta+ = delta + dt w
+    xn[0] = z[ZX] + dX.v;
+    xn[1] = z[ZY] + dY.v;
+    xn[2] = psi.v;
+    xn[3] = z[ZV] + pr.dt * z[ZA];
+    xn[4] = z[ZDELTA] + pr.dt * z[ZW];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < NZB; ++j) F[i][j] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        F[0][ri[j]] = dX.g[j];
+        F[1][ri[j]] = dY.g[j];
+        F[2][ri[j]] = psi.g[j];
+    }
+    F[0][ZX] = 1.0;
+    F[1][ZY] = 1.0;
+    F[3][ZV] = 1.0; F[3][ZA] = pr.dt;
+    F[4][ZDELTA] = 1.0; F[4][ZW] = pr.dt;
+    const double p2 = pi ? pi[2] : 0.0;
+#pragma unroll
+    for (int i = 0; i < NZB * (NZB + 1) / 2; ++i) Hp[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Hp[tri(ri[i], ri[j])] = p2 * psi.h[tri(i, j)];
+
     // ---- CA spline update (solver_model.py:409-437); local jets 0 x, 1 y, 2 s, 3 dpx, 4 dpy
     PathJets PJ;
     path_jets(pr, p, z[ZS], PJ);
@@ -282,72 +310,35 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
     const J5 vt = dpx * tx + dpy * ty;                                         // (:429)
     const J5 vn = dpx * ty - dpy * tx;                                         // (:430)
     const J5 G = jvar(2, z[ZS]) + R * jatan2(vt, R - ec - vn);                 // (:435-437)
-
-    xn[0] = z[ZX] + dX.v;
-    xn[1] = z[ZY] + dY.v;
-    xn[2] = psi.v;
-    xn[3] = v.v;
-    xn[4] = del.v;
     xn[5] = G.v;
 #pragma unroll
-    for (int i = 0; i < NXB; ++i)
+    for (int j = 0; j < NZB; ++j) F[5][j] = 0.0;
 #pragma unroll
-        for (int j = 0; j < NZB; ++j) F[i][j] = 0.0;
-    constexpr int ri[5] = {ZA, ZW, ZPSI, ZV, ZDELTA};
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        F[0][ri[j]] = dX.g[j];
-        F[1][ri[j]] = dY.g[j];
-        F[2][ri[j]] = psi.g[j];
-        F[3][ri[j]] = v.g[j];
-        F[4][ri[j]] = del.g[j];
-        F[5][ri[j]] = G.g[3] * dX.g[j] + G.g[4] * dY.g[j];
-    }
-    F[0][ZX] = 1.0;
-    F[1][ZY] = 1.0;
+    for (int j = 0; j < 5; ++j) F[5][ri[j]] = G.g[3] * dX.g[j] + G.g[4] * dY.g[j];
     F[5][ZX] = G.g[0];
     F[5][ZY] = G.g[1];
     F[5][ZS] = G.g[2];
     if (!pi) return;
     const double ps = pi[5];
     const double cX = pi[0] + ps * G.g[3], cY = pi[1] + ps * G.g[4];
-    // (a, w, psi, v, delta) block: second derivatives of the integrated states
+    // (a, w, psi, v, delta) block: second derivatives of dX, dY and the update's (dpx, dpy) block
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < 5; ++i) {
+        const double gxi = ps * (G.h[tri(3, 3)] * dX.g[i] + G.h[tri(4, 3)] * dY.g[i]);
+        const double gyi = ps * (G.h[tri(4, 3)] * dX.g[i] + G.h[tri(4, 4)] * dY.g[i]);
 #pragma unroll
-        for (int j = 0; j <= i; ++j) {
-            const double hv = cX * dX.h[tri(i, j)] + cY * dY.h[tri(i, j)] + pi[2] * psi.h[tri(i, j)];
-            H[ri[i]][ri[j]] += hv;
-            if (i != j) H[ri[j]][ri[i]] += hv;
-        }
-    // ps * W' Hess(G) W with W: x -> e_x, y -> e_y, s -> e_s, dpx -> dX.g, dpy -> dY.g
-    double Wm[5][NZB];
-#pragma unroll
-    for (int m = 0; m < 5; ++m)
-#pragma unroll
-        for (int j = 0; j < NZB; ++j) Wm[m][j] = 0.0;
-    Wm[0][ZX] = 1.0;
-    Wm[1][ZY] = 1.0;
-    Wm[2][ZS] = 1.0;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        Wm[3][ri[j]] = dX.g[j];
-        Wm[4][ri[j]] = dY.g[j];
+        for (int j = 0; j <= i; ++j)
+            Hp[tri(ri[i], ri[j])] += cX * dX.h[tri(i, j)] + cY * dY.h[tri(i, j)] + gxi * dX.g[j] + gyi * dY.g[j];
     }
-    if (ps != 0.0) {
+    // (x, y, s) block and its coupling with (a, w, psi, v, delta) through (dpx, dpy)
+    constexpr int ui[3] = {ZX, ZY, ZS};
 #pragma unroll
-        for (int i = 0; i < NZB; ++i)
+    for (int m = 0; m < 3; ++m) {
 #pragma unroll
-            for (int j = 0; j <= i; ++j) {
-                double acc = 0.0;
+        for (int n = 0; n <= m; ++n) Hp[tri(ui[m], ui[n])] += ps * G.h[tri(m, n)];
+        const double c3 = ps * G.h[tri(3, m)], c4 = ps * G.h[tri(4, m)];
 #pragma unroll
-                for (int m = 0; m < 5; ++m)
-#pragma unroll
-                    for (int n = 0; n < 5; ++n) acc += Wm[m][i] * G.h[tri(m, n)] * Wm[n][j];
-                acc *= ps;
-                H[i][j] += acc;
-                if (i != j) H[j][i] += acc;
-            }
+        for (int j = 0; j < 5; ++j) Hp[tri(ui[m], ri[j])] += c3 * dX.g[j] + c4 * dY.g[j];
     }
 }
 

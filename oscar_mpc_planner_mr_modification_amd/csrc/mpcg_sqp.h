@@ -415,22 +415,41 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             }
             double resl = 0.0;
             if (stage_lane && k < N) {
-                double g[NZ], H[NZ][NZ], F[NX][NZ], xn[NX], pi[NX];
-                if constexpr (C::MODEL == 1) bike::stage_cost(pr, pk, k, zk, g, H, true);
-                else stage_cost<NX>(pr, pk, zk, g, H, true);
-                STAMP_LAP(11);
+                double g[NZ], H[NZ][NZ], xn[NX], pi[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
-                if constexpr (C::MODEL == 1) bike::discrete(pr, pk, zk, pi, xn, F, H);
-                else erk_unicycle<NX>(pr, zk, pi, xn, F, H);
-                STAMP_LAP(12);
+                if constexpr (C::MODEL == 1) {
+                    // the bicycle: the discrete map first (F straight to LDS, its Hessian packed),
+                    // then the cost, so that the map's jets and the 9x9 cost block are not live together
+                    double Hp[C::NTRI];
+                    bike::discrete(pr, pk, zk, pi, xn, S.F[k], Hp);
+                    STAMP_LAP(12);
+                    bike::stage_cost(pr, pk, k, zk, g, H, true);
+                    STAMP_LAP(11);
 #pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    const double bi = xn[i] - S.z[k + 1][NU + i];
-                    S.b[k][i] = bi;
-                    resl = fmax(resl, fabs(bi));
+                    for (int i = 0; i < NZ; ++i)
 #pragma unroll
-                    for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                        for (int j = 0; j < NZ; ++j) H[i][j] += Hp[sym(i, j)];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        const double bi = xn[i] - S.z[k + 1][NU + i];
+                        S.b[k][i] = bi;
+                        resl = fmax(resl, fabs(bi));
+                    }
+                } else {
+                    double F[NX][NZ];
+                    stage_cost<NX>(pr, pk, zk, g, H, true);
+                    STAMP_LAP(11);
+                    erk_unicycle<NX>(pr, zk, pi, xn, F, H);
+                    STAMP_LAP(12);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        const double bi = xn[i] - S.z[k + 1][NU + i];
+                        S.b[k][i] = bi;
+                        resl = fmax(resl, fabs(bi));
+#pragma unroll
+                        for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) S.g[k][i] = g[i];
