@@ -218,16 +218,17 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
 
 // ---------------------------------------------------------------------------
 // Discrete map of one shooting interval: RK4 (pr.rk_steps steps over dt) of the
-// five bicycle states, then the CA spline update.  Outputs xn, F = [B A]
-// (nx x nz, written straight to `F`, LDS in the kernel) and Hp = Hess(pi' x+)
-// packed (lower triangle over z, sym index).
+// five bicycle states, then the CA spline update.  Outputs xn, the rows of
+// [B A] of x+, y+, psi+ and s+ without the slack column (written straight to
+// `F`, LDS in the kernel; the rows of v+ = v + dt a and delta+ = delta + dt w
+// are known) and Hp = Hess(pi' x+) packed (lower triangle over z, sym index).
 // RK jets over 0 a, 1 w, 2 psi, 3 v, 4 delta; x and y enter the integrated
 // positions additively (x+ = x + dX, y+ = y + dY), so dp = (dX, dY) in the update.
 // Written to keep few jets live at once (the linearisation lane's registers):
 // F rows and the psi Hessian leave before the update is evaluated.
 // ---------------------------------------------------------------------------
 __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict__ p, const double z[NZB],
-                                const double* pi, double xn[NXB], double (*F)[NZB], double Hp[NZB * (NZB + 1) / 2]) {
+                                const double* pi, double xn[NXB], double (*F)[NZB - 1], double Hp[NZB * (NZB + 1) / 2]) {
     const int ns = pr.rk_steps;
     const double h = pr.dt / ns;
     // v' = a and delta' = w are integrated exactly (v_q = v + tau a, delta_q = delta + tau w at
@@ -270,20 +271,20 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
     xn[2] = psi.v;
     xn[3] = z[ZV] + pr.dt * z[ZA];
     xn[4] = z[ZDELTA] + pr.dt * z[ZW];
+    // compact column of z variable j (the slack column is not stored)
+    constexpr auto fc = [](int j) { return j < ZSL ? j : j - 1; };
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < NZB; ++j) F[i][j] = 0.0;
+        for (int j = 0; j < NZB - 1; ++j) F[i][j] = 0.0;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-        F[0][ri[j]] = dX.g[j];
-        F[1][ri[j]] = dY.g[j];
-        F[2][ri[j]] = psi.g[j];
+        F[0][fc(ri[j])] = dX.g[j];
+        F[1][fc(ri[j])] = dY.g[j];
+        F[2][fc(ri[j])] = psi.g[j];
     }
-    F[0][ZX] = 1.0;
-    F[1][ZY] = 1.0;
-    F[3][ZV] = 1.0; F[3][ZA] = pr.dt;
-    F[4][ZDELTA] = 1.0; F[4][ZW] = pr.dt;
+    F[0][fc(ZX)] = 1.0;
+    F[1][fc(ZY)] = 1.0;
     const double p2 = pi ? pi[2] : 0.0;
 #pragma unroll
     for (int i = 0; i < NZB * (NZB + 1) / 2; ++i) Hp[i] = 0.0;
@@ -312,12 +313,12 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
     const J5 G = jvar(2, z[ZS]) + R * jatan2(vt, R - ec - vn);                 // (:435-437)
     xn[5] = G.v;
 #pragma unroll
-    for (int j = 0; j < NZB; ++j) F[5][j] = 0.0;
+    for (int j = 0; j < NZB - 1; ++j) F[3][j] = 0.0;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) F[5][ri[j]] = G.g[3] * dX.g[j] + G.g[4] * dY.g[j];
-    F[5][ZX] = G.g[0];
-    F[5][ZY] = G.g[1];
-    F[5][ZS] = G.g[2];
+    for (int j = 0; j < 5; ++j) F[3][fc(ri[j])] = G.g[3] * dX.g[j] + G.g[4] * dY.g[j];
+    F[3][fc(ZX)] = G.g[0];
+    F[3][fc(ZY)] = G.g[1];
+    F[3][fc(ZS)] = G.g[2];
     if (!pi) return;
     const double ps = pi[5];
     const double cX = pi[0] + ps * G.g[3], cY = pi[1] + ps * G.g[4];

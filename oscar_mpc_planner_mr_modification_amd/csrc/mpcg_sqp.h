@@ -103,6 +103,13 @@ struct Cfg {
     }
     // z variable of block index b
     __host__ __device__ static constexpr int bvar(int b) { return b < 3 ? IX + b : ZSL; }
+    // C3 storage (LDS under the 3-solves-per-CU line): the bicycle's [B A] keeps the rows of
+    // x+, y+, psi+, s+ without the slack column (v+ = v + dt a, delta+ = delta + dt w are
+    // known), its Hessian block drops the slack row / column but the diagonal, and the new
+    // dynamics multipliers and the dynamics residuals live in registers / are recomputed
+    static constexpr bool COMPACT = MODEL_ == 1;
+    static constexpr int NFR = COMPACT ? 4 : NX, NFC = COMPACT ? NZ - 1 : NZ;
+    static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -111,9 +118,9 @@ template <class C>
 struct Lds {
     static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
     double z[N + 1][NZ];      // NLP iterate [u x]
-    double H[N + 1][C::NTRI]; // MIRROR-regularised Lagrangian Hessian, packed lower triangle
+    double H[N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
     double g[N + 1][NZ];
-    double F[N][NX][NZ];      // [B A]
+    double F[N][C::NFR][C::NFC];  // [B A] (C::COMPACT: rows x+ y+ psi+ s+, no slack column)
     double b[N][NX];          // shooting defects
     double dH[N + 1][C::NDH]; // barrier terms: diag(nz) + h-row block (column-major packed), last = 0
     double q[N + 1][NZ];      // Newton gradient
@@ -121,8 +128,8 @@ struct Lds {
     double ddz[N + 1][NZ];    // QP step
     double pi_nlp[N][NX];
     double piq[N][NX];
-    double pin[N][NX];
-    double rdyn[N][NX];
+    double pin[C::COMPACT ? 1 : N][NX];
+    double rdyn[C::COMPACT ? 1 : N][NX];
     double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
     double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
@@ -370,6 +377,33 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             return S.hd[k][hh];
         }
     };
+    // [B A] and Hessian entries of stage kq (the compact C3 storage rebuilds the known ones)
+    auto Fat = [&](int kq, int m, int j) -> double {
+        if constexpr (C::COMPACT) {
+            if (m == 3) return j == bike::ZV ? 1.0 : (j == bike::ZA ? pr.dt : 0.0);
+            if (m == 4) return j == bike::ZDELTA ? 1.0 : (j == bike::ZW ? pr.dt : 0.0);
+            if (j == ZS) return 0.0;
+            return S.F[kq][m < 3 ? m : 3][j < ZS ? j : j - 1];
+        } else {
+            return S.F[kq][m][j];
+        }
+    };
+    auto Hat = [&](int kq, int i, int j) -> double {
+        if constexpr (C::COMPACT) {
+            if (i == ZS || j == ZS) return (i == j) ? S.H[kq][C::NHP - 1] : 0.0;
+            return S.H[kq][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
+        } else {
+            return S.H[kq][sym(i, j)];
+        }
+    };
+    // dynamics residual b + F dz - dz+ of stage kq at the current QP iterate (same operation order
+    // as the residual phase, which stores it unless C::COMPACT)
+    auto rdyn_at = [&](int kq, int i) -> double {
+        double a = S.b[kq][i] - S.dz[kq + 1][NU + i];
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) a += Fat(kq, i, j) * S.dz[kq][j];
+        return a;
+    };
     Rows<C> R;
 #pragma unroll
     for (int r = 0; r < HS; ++r) R.nlam[r] = (lam_in && LR.h_on(r)) ? lam_in[(size_t)k * LAMS + NX + LR.hrow(r)] : 0.0;
@@ -495,16 +529,28 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     mirror<NZ>(H, pr.reg_eps);
                 }
                 STAMP_LAP(14);
+                if constexpr (C::COMPACT) {
 #pragma unroll
-                for (int i = 0; i < NZ; ++i)
+                    for (int i = 0; i < NZ; ++i)
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) S.H[k][sym(i, j)] = H[i][j];
+                        for (int j = 0; j <= i; ++j)
+                            if (i != ZS && j != ZS) S.H[k][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)] = H[i][j];
+                    S.H[k][C::NHP - 1] = H[ZS][ZS];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NZ; ++i)
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) S.H[k][sym(i, j)] = H[i][j];
+                }
             } else if (stage_lane && k == N) {
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) {
-                    S.g[N][i] = 0.0;
+                for (int i = 0; i < NZ; ++i) S.g[N][i] = 0.0;
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) S.H[N][sym(i, j)] = (i == j && i >= NU) ? pr.reg_eps : 0.0;
+                for (int e = 0; e < C::NHP; ++e) S.H[N][e] = 0.0;
+#pragma unroll
+                for (int i = NU; i < NZ; ++i) {
+                    if constexpr (C::COMPACT) S.H[N][sym(i - 1, i - 1)] = pr.reg_eps;
+                    else S.H[N][sym(i, i)] = pr.reg_eps;
                 }
             }
             res_eq = wave_max(resl);
@@ -551,6 +597,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         __syncthreads();
         STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
+        double pinr[C::COMPACT ? NX : 1];  // C::COMPACT: the new dynamics multipliers of the own stage
         double Hdz[NZ];  // part 0: H_k dz_k of the current iterate
         for (;; ++qit) {
             if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
@@ -627,7 +674,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     for (int i = 0; i < NZ; ++i) {
                         double a = 0.0;
 #pragma unroll
-                        for (int j = 0; j < NZ; ++j) a += S.H[k][sym(i, j)] * dzk[j];
+                        for (int j = 0; j < NZ; ++j) a += Hat(k, i, j) * dzk[j];
                         Hdz[i] = a;
                         r[i] = a + S.g[k][i] + rbox[i];
                     }
@@ -636,14 +683,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int m = 0; m < NX; ++m) {
                             const double pm = S.piq[k][m];
 #pragma unroll
-                            for (int i = 0; i < NZ; ++i) r[i] += S.F[k][m][i] * pm;
+                            for (int i = 0; i < NZ; ++i) r[i] += Fat(k, m, i) * pm;
                         }
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             double a = S.b[k][i] - S.dz[k + 1][NU + i];
 #pragma unroll
-                            for (int j = 0; j < NZ; ++j) a += S.F[k][i][j] * dzk[j];
-                            S.rdyn[k][i] = a;
+                            for (int j = 0; j < NZ; ++j) a += Fat(k, i, j) * dzk[j];
+                            if constexpr (!C::COMPACT) S.rdyn[k][i] = a;
                             re = fmax(re, fabs(a));
                         }
                     }
@@ -766,15 +813,21 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     int pi_ = 0;
                     while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < NX - 1) ++pi_;
                     const int pj_ = lane < NP ? lane - pi_ * (pi_ + 1) / 2 : 0;
-                    if (lane < NP) S.P[N][lane] = S.H[N][sym(NU + pi_, NU + pj_)] + dh_at<C>(S.dH[N], NU + pi_, NU + pj_);
+                    if (lane < NP) S.P[N][lane] = Hat(N, NU + pi_, NU + pj_) + dh_at<C>(S.dH[N], NU + pi_, NU + pj_);
                     if (lane == 0) S.flag = 0;
                     __syncthreads();
                     // prefetch of stage N-1's block
                     const int le = lane < NT ? lane : 0;
                     double fi[NX], fj[NX], hv;
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) { fi[m] = S.F[N - 1][m][ei]; fj[m] = S.F[N - 1][m][ej]; }
-                    hv = S.H[N - 1][le] + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
+                    for (int m = 0; m < NX; ++m) { fi[m] = Fat(N - 1, m, ei); fj[m] = Fat(N - 1, m, ej); }
+                    // packed Hessian entry of the element lane (the compact storage: slack row / column 0
+                    // but the diagonal)
+                    auto Hel = [&](int kq) -> double {
+                        if constexpr (C::COMPACT) return Hat(kq, ei, ej);
+                        else return S.H[kq][le];
+                    };
+                    hv = Hel(N - 1) + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
 #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
                         double Pm[NP];
@@ -784,8 +837,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const int kn = kk > 0 ? kk - 1 : 0;
                         double fi2[NX], fj2[NX];
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) { fi2[m] = S.F[kn][m][ei]; fj2[m] = S.F[kn][m][ej]; }
-                        const double hv2 = S.H[kn][le] + S.dH[kn][dhd] + S.dH[kn][dhb];
+                        for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
+                        const double hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
                         double v = hv;
 #pragma unroll
                         for (int m = 0; m < NX; ++m) {
@@ -888,10 +941,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
                     }
                     double G[NX][NX], hv[NX], Wu[NU][NX], y0[NU];
+                    double rdv[C::COMPACT ? NX : 1];  // C::COMPACT: recomputed dynamics residual
                     {
                         double c[NX], rr[NX];
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) rr[i] = S.rdyn[kq][i];
+                        for (int i = 0; i < NX; ++i) {
+                            if constexpr (C::COMPACT) rr[i] = rdv[i] = rdyn_at(kq, i);
+                            else rr[i] = S.rdyn[kq][i];
+                        }
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             double a = 0.0;
@@ -904,7 +961,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int i = 0; i < NZ; ++i) {
                             double a = S.q[kq][i];
 #pragma unroll
-                            for (int j = 0; j < NX; ++j) a += S.F[kq][j][i] * c[j];
+                            for (int j = 0; j < NX; ++j) a += Fat(kq, j, i) * c[j];
                             m0[i] = a;
                         }
 #pragma unroll
@@ -922,7 +979,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             hv[i] = acc;
 #pragma unroll
                             for (int u = 0; u < NU; ++u) {
-                                double w = S.F[kq][i][u];
+                                double w = Fat(kq, i, u);
 #pragma unroll
                                 for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wu[m][i];
                                 Wu[u][i] = w * il[u];
@@ -935,7 +992,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int u = 0; u < NU; ++u) Yi[u] = S.Y[kq][u][i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) {
-                                double acc = S.F[kq][j][NU + i];
+                                double acc = Fat(kq, j, NU + i);
 #pragma unroll
                                 for (int u = 0; u < NU; ++u) acc -= Yi[u] * Wu[u][j];
                                 G[i][j] = acc;
@@ -984,9 +1041,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double e[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
-                        double acc = S.rdyn[kq][i];
+                        double acc;
+                        if constexpr (C::COMPACT) acc = rdv[i];
+                        else acc = S.rdyn[kq][i];
 #pragma unroll
-                        for (int u = 0; u < NU; ++u) acc += S.F[kq][i][u] * kf[u];
+                        for (int u = 0; u < NU; ++u) acc += Fat(kq, i, u) * kf[u];
                         e[i] = acc;
                     }
                     double dxu[NX], dxmine[NX];
@@ -1041,7 +1100,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            S.pin[k][i] = a;
+                            if constexpr (C::COMPACT) pinr[i] = a;
+                            else S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
 #pragma unroll
@@ -1148,7 +1208,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < NZ; ++i) S.dz[k][i] += alpha * S.ddz[k][i];
                 if (k < N) {
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
+                    for (int i = 0; i < NX; ++i) {
+                        if constexpr (C::COMPACT) S.piq[k][i] += alpha * (pinr[i] - S.piq[k][i]);
+                        else S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
+                    }
                 }
             }
             __syncthreads();
