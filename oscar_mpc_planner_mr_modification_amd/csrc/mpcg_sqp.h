@@ -133,13 +133,15 @@ struct Lds {
     double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
     double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
-    double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane
+    double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane;
+                              // dead from the Newton gradient to the next residuals: holds the
+                              // backward vector chain p_k [N][NX] meanwhile
     double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
     double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
     double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
     double Msc[C::NTRI];      // factorisation scratch
     double xinit[NX];
-    int flag;
+    int flag;                 // failed pivot (C::COMPACT; the others vote in registers)
 };
 
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
@@ -814,7 +816,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < NX - 1) ++pi_;
                     const int pj_ = lane < NP ? lane - pi_ * (pi_ + 1) / 2 : 0;
                     if (lane < NP) S.P[N][lane] = Hat(N, NU + pi_, NU + pj_) + dh_at<C>(S.dH[N], NU + pi_, NU + pj_);
-                    if (lane == 0) S.flag = 0;
+                    // failed pivots accumulate in a register and are voted once after the
+                    // recursion (a store under a branch inside the stage loop kept the
+                    // scheduler from hoisting the next LDS reads over it).  The register-starved
+                    // bicycle instance keeps the LDS flag: there the hoisted reads spill.
+                    bool fbad = false;
+                    if (C::COMPACT && lane == 0) S.flag = 0;
                     __syncthreads();
                     // prefetch of stage N-1's block
                     const int le = lane < NT ? lane : 0;
@@ -863,7 +870,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             const double l10 = m10 * il00;
                             const double r11 = m11 - l10 * l10;
                             const double il11 = frsq(r11);
-                            if (!(m00 > 0.0) || !(r11 > 0.0)) S.flag = 1;
+                            fbad = fbad | !(m00 > 0.0) | !(r11 > 0.0);
                             const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
                             const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
                             const double y0j = S.Msc[sym(NU + pj_, 0)] * il00;
@@ -892,7 +899,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                                     Lm[i][j] = acc * il[j];
                                 }
                             }
-                            if (bad) S.flag = 1;
+                            if constexpr (C::COMPACT) {
+                                if (bad) S.flag = 1;
+                            } else {
+                                fbad = fbad | bad;
+                            }
                             double yi[NU], yj[NU];
 #pragma unroll
                             for (int u = 0; u < NU; ++u) {
@@ -923,7 +934,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         __syncthreads();
                         STAMP_LAP(19);
                     }
-                    if (S.flag) { qstat = AC_NAN; break; }
+                    if (C::COMPACT ? S.flag != 0 : __any(fbad)) { qstat = AC_NAN; break; }
                 }
                 STAMP_END(4);
                 // ---- vector + forward passes: affine 5-vector recursions in SGPRs
@@ -999,11 +1010,17 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             }
                         }
                     }
+                    // each chain step's value is recorded in LDS by the lane that owns it (a
+                    // predicated store off the VALU path) and read back after the chain; the
+                    // register-starved bicycle instance selects it into registers instead
+                    constexpr bool CHAIN_REC = !C::COMPACT;
                     double pu[NX], pmine[NX];
+                    double* const pch = &S.bx[0][0];
+                    static_assert((N + 1) * NZ >= N * NX, "chain storage");
 #pragma unroll
                     for (int i = 0; i < NX; ++i) { pu[i] = S.q[N][NU + i]; pmine[i] = pu[i]; }
                     #pragma unroll
-                    for (int kk = N - 1; kk >= 0; --kk) {
+                    for (int kk = N - 1; kk >= 1; --kk) {  // p_0 is not needed
                         double pn[NX];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
@@ -1012,12 +1029,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += G[i][j] * pu[j];
                             pn[i] = a;
                         }
-                        const bool mine = (k == kk) && (part == 0);
+                        if (CHAIN_REC && lane == kk * PARTS) {
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) pch[kk * NX + i] = pn[i];
+                        }
+                        const bool mine = !CHAIN_REC && (k == kk - 1) && (part == 0);
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            pmine[i] = mine ? pu[i] : pmine[i];
                             pu[i] = readlane_d(pn[i], kk * PARTS);
+                            if constexpr (!CHAIN_REC) pmine[i] = mine ? pu[i] : pmine[i];
                         }
+                    }
+                    if constexpr (CHAIN_REC) {
+                        __syncthreads();
+                        const double* src = (kq + 1 < N) ? pch + (kq + 1) * NX : &S.q[N][NU];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) pmine[i] = src[i];
                     }
                     // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
                     double kf[NU];
@@ -1048,11 +1075,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int u = 0; u < NU; ++u) acc += Fat(kq, i, u) * kf[u];
                         e[i] = acc;
                     }
+                    // dx_{kk+1} goes straight to its place in the QP step, ddz[kk + 1]
                     double dxu[NX], dxmine[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) { dxu[i] = 0.0; dxmine[i] = 0.0; }
                     #pragma unroll
-                    for (int kk = 0; kk < N; ++kk) {
+                    for (int kk = 0; kk < N - 1; ++kk) {  // dx_N comes from stage N - 1's own lane
                         double dn[NX];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
@@ -1061,12 +1089,21 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += G[j][i] * dxu[j];
                             dn[i] = a;
                         }
-                        const bool mine = (k == kk) && (part == 0);
+                        if (CHAIN_REC && lane == kk * PARTS) {
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) S.ddz[kk + 1][NU + i] = dn[i];
+                        }
+                        const bool mine = !CHAIN_REC && (k == kk + 1) && (part == 0);
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            dxmine[i] = mine ? dxu[i] : dxmine[i];
                             dxu[i] = readlane_d(dn[i], kk * PARTS);
+                            if constexpr (!CHAIN_REC) dxmine[i] = mine ? dxu[i] : dxmine[i];
                         }
+                    }
+                    if constexpr (CHAIN_REC) {
+                        __syncthreads();
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) dxmine[i] = (k >= 1 && k < N) ? S.ddz[k][NU + i] : 0.0;
                     }
                     if (own) {
                         double du[NU], dxn[NX];
@@ -1096,7 +1133,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int u = 0; u < NU; ++u) S.ddz[k][u] = du[u];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            S.ddz[k][NU + i] = (k == 0) ? 0.0 : dxmine[i];
+                            if (!CHAIN_REC || k == 0) S.ddz[k][NU + i] = dxmine[i];  // 0 at k = 0
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
