@@ -139,7 +139,8 @@ struct Lds {
     double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
     double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
     double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
-    double Msc[C::NTRI];      // factorisation scratch
+    double Msc[128];          // factorisation scratch: the stage block (lanes < nz(nz+1)/2) and
+                              // dummy targets (64 + lane) of the branch-free stores
     double xinit[NX];
     int flag;                 // failed pivot (C::COMPACT; the others vote in registers)
 };
@@ -800,6 +801,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 STAMP_BEGIN();
                 if (phase == 0) {
                     constexpr int NT = C::NTRI, NP = C::NPT, DZ = C::NDH - 1;
+                    constexpr bool FAC_FLAT = !C::COMPACT;
                     // element lane -> (ei, ej), ei >= ej, of the nz x nz block
                     int ei = 0;
                     while ((ei + 1) * (ei + 2) / 2 <= lane && ei < NZ - 1) ++ei;
@@ -840,43 +842,72 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         double Pm[NP];
 #pragma unroll
                         for (int e = 0; e < NP; ++e) Pm[e] = S.P[kk + 1][e];
-                        // prefetch the next (lower) stage's block; it lands while this one is reduced
+                        // prefetch of the next (lower) stage's block; it lands while this one is
+                        // reduced.  FAC_FLAT: every lane runs one branch-free block, the five row
+                        // products advance together, and the prefetch is issued after the pivot
+                        // block's reads (off the recursion's critical path, and not in front of
+                        // the LDS traffic the next step waits for)
+                        static_assert(!FAC_FLAT || NU == 2, "flat factorisation: 2 inputs");
                         const int kn = kk > 0 ? kk - 1 : 0;
-                        double fi2[NX], fj2[NX];
+                        double fi2[NX], fj2[NX], hv2;
+                        auto prefetch = [&]() {
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
-                        const double hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
+                            for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
+                            hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
+                        };
+                        if constexpr (!FAC_FLAT) prefetch();
                         double v = hv;
+                        if constexpr (FAC_FLAT) {
+                            double tm[NX];
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) {
-                            double tm = 0.0;
+                            for (int m = 0; m < NX; ++m) tm[m] = 0.0;
 #pragma unroll
-                            for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
-                            v += fi[m] * tm;
+                            for (int l = 0; l < NX; ++l)
+#pragma unroll
+                                for (int m = 0; m < NX; ++m) tm[m] += Pm[sym(m, l)] * fj[l];
+#pragma unroll
+                            for (int m = 0; m < NX; ++m) v += fi[m] * tm[m];
+                            S.Msc[lane < NT ? lane : 64 + lane] = v;
+                        } else {
+#pragma unroll
+                            for (int m = 0; m < NX; ++m) {
+                                double tm = 0.0;
+#pragma unroll
+                                for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
+                                v += fi[m] * tm;
+                            }
+                            if (lane < NT) S.Msc[lane] = v;
                         }
-                        if (lane < NT) S.Msc[lane] = v;
-#pragma unroll
-                        for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
-                        hv = hv2;
                         STAMP_LAP(16);
                         __syncthreads();
                         STAMP_LAP(17);
                         if constexpr (NU == 2) {
-                          if (lane < NP) {
+                          if (FAC_FLAT || lane < NP) {
                             const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
+                            const double mi0 = S.Msc[sym(NU + pi_, 0)], mi1 = S.Msc[sym(NU + pi_, 1)];
+                            const double mj0 = S.Msc[sym(NU + pj_, 0)], mj1 = S.Msc[sym(NU + pj_, 1)];
+                            const double mij = S.Msc[sym(NU + pi_, NU + pj_)];
+                            if constexpr (FAC_FLAT) {
+                                __builtin_amdgcn_sched_barrier(0);
+                                prefetch();
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
                             // 2x2 Cholesky through reciprocal square roots
+                            // 1/l11 = sqrt(m00 / det) = l00 / sqrt(det): both reciprocal square
+                            // roots start from the block entries and run side by side
                             const double il00 = frsq(m00);
+                            const double det = fma(m00, m11, -(m10 * m10));
+                            const double ild = frsq(det);
                             const double l00 = m00 * il00;
                             const double l10 = m10 * il00;
-                            const double r11 = m11 - l10 * l10;
-                            const double il11 = frsq(r11);
-                            fbad = fbad | !(m00 > 0.0) | !(r11 > 0.0);
-                            const double y0i = S.Msc[sym(NU + pi_, 0)] * il00;
-                            const double y1i = (S.Msc[sym(NU + pi_, 1)] - l10 * y0i) * il11;
-                            const double y0j = S.Msc[sym(NU + pj_, 0)] * il00;
-                            const double y1j = (S.Msc[sym(NU + pj_, 1)] - l10 * y0j) * il11;
-                            S.P[kk][lane] = S.Msc[sym(NU + pi_, NU + pj_)] - y0i * y0j - y1i * y1j;
-                            if (pj_ == 0) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
+                            const double il11 = l00 * ild;
+                            fbad = fbad | !(m00 > 0.0) | !(det > 0.0);
+                            const double y0i = mi0 * il00;
+                            const double y1i = (mi1 - l10 * y0i) * il11;
+                            const double y0j = mj0 * il00;
+                            const double y1j = (mj1 - l10 * y0j) * il11;
+                            *(lane < NP ? &S.P[kk][lane] : &S.Msc[64 + lane]) = mij - y0i * y0j - y1i * y1j;
+                            if (pj_ == 0 && lane < NP) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
                             if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
                           }
                         } else if (lane < NP) {
@@ -930,6 +961,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                                 for (int u = 0; u < NU; ++u) S.Lc[kk][C::NLO + u] = il[u];
                             }
                         }
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
+                        hv = hv2;
                         STAMP_LAP(18);
                         __syncthreads();
                         STAMP_LAP(19);
@@ -1010,6 +1044,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             }
                         }
                     }
+                    STAMP_LAP(6);
                     // each chain step's value is recorded in LDS by the lane that owns it (a
                     // predicated store off the VALU path) and read back after the chain; the
                     // register-starved bicycle instance selects it into registers instead
@@ -1046,6 +1081,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                         for (int i = 0; i < NX; ++i) pmine[i] = src[i];
                     }
+                    STAMP_LAP(15);
                     // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
                     double kf[NU];
                     {
@@ -1105,6 +1141,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                         for (int i = 0; i < NX; ++i) dxmine[i] = (k >= 1 && k < N) ? S.ddz[k][NU + i] : 0.0;
                     }
+                    STAMP_LAP(9);
                     if (own) {
                         double du[NU], dxn[NX];
 #pragma unroll

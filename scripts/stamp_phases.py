@@ -13,8 +13,8 @@ from oscar_mpc_planner_mr_modification_amd import native  # noqa: E402
 from oscar_mpc_planner_mr_modification_amd.layouts import config_layout  # noqa: E402
 from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch  # noqa: E402
 
-PH = ["linearize", "qp_init", "residuals", "barrier_q", "factor", "vec+fwd", "-", "steps+rowupd", "update", "output",
-      "lin:h_rows", "lin:cost", "lin:erk", "lin:store", "lin:mirror", "-",
+PH = ["linearize", "qp_init", "residuals", "barrier_q", "factor", "vec+fwd", "vf:pre", "steps+rowupd", "update",
+      "vf:fwd", "lin:h_rows", "lin:cost", "lin:erk", "lin:store", "lin:mirror", "vf:bwd",
       "fac:elem", "fac:sync1", "fac:chol", "fac:sync2"]
 NS = len(PH)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
