@@ -110,6 +110,9 @@ struct Cfg {
     static constexpr bool COMPACT = MODEL_ == 1;
     static constexpr int NFR = COMPACT ? 4 : NX, NFC = COMPACT ? NZ - 1 : NZ;
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
+    // the vector chains split over the parts of a stage (rows of the backward map, columns of
+    // the forward one); the register-starved bicycle instance keeps one owner per stage
+    static constexpr bool CHAIN_SPLIT = !COMPACT;
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -973,6 +976,219 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 STAMP_END(4);
                 // ---- vector + forward passes: affine 5-vector recursions in SGPRs
                 STAMP_BEGIN();
+                if constexpr (C::CHAIN_SPLIT) {
+                    static_assert(NU == 2, "split chains: 2 inputs");
+                    // Every part of stage k owns the rows {part + PARTS s} of the stage's
+                    // backward map p_k = h_k + G_k p_{k+1} and the same columns of the forward
+                    // map dx_{k+1} = G_k' dx_k + e_k: a chain step is RS short dot products per
+                    // lane instead of one whole 5x5 product, and the owning parts' rows meet
+                    // in SGPRs through v_readlane.  Same operation order per row as the
+                    // single-owner chain (bit-identical).
+                    constexpr int RS = (NX + PARTS - 1) / PARTS;
+                    const int kv = k < N ? k : 0;
+                    const bool own = stage_lane && k < N;
+                    double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
+                    Lo[0] = S.Lc[kv][1]; il[0] = S.Lc[kv][2]; il[1] = S.Lc[kv][3];
+                    int rs[RS];
+                    bool rv[RS];
+#pragma unroll
+                    for (int t = 0; t < RS; ++t) {
+                        rv[t] = part + PARTS * t < NX;
+                        rs[t] = rv[t] ? part + PARTS * t : NX - 1;
+                    }
+                    double Wu[NU][NX], y0[NU], c[NX];
+                    {
+                        double rr[NX];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rr[i] = S.rdyn[kv][i];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            double a = 0.0;
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) a += S.P[kv + 1][sym(i, j)] * rr[j];
+                            c[i] = a;
+                        }
+                        double m0u[NU];
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) {
+                            double a = S.q[kv][i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) a += Fat(kv, j, i) * c[j];
+                            m0u[i] = a;
+                        }
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            double acc = m0u[u];
+#pragma unroll
+                            for (int m = 0; m < u; ++m) acc -= Lo[C::lo_idx(u, m)] * y0[m];
+                            y0[u] = acc * il[u];
+                        }
+#pragma unroll
+                        for (int i = 0; i < NX; ++i)
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) {
+                                double w = Fat(kv, i, u);
+#pragma unroll
+                                for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wu[m][i];
+                                Wu[u][i] = w * il[u];
+                            }
+                    }
+                    // my rows of the backward map (h_r, G[r][.]) and columns of the forward one
+                    double hr[RS], Gr[RS][NX], Gc[RS][NX];
+#pragma unroll
+                    for (int t = 0; t < RS; ++t) {
+                        const int r = rs[t];
+                        double a = S.q[kv][NU + r];
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) a += Fat(kv, j, NU + r) * c[j];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) a -= S.Y[kv][u][r] * y0[u];
+                        hr[t] = a;
+                        double Yr[NU], Wr[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) Yr[u] = S.Y[kv][u][r];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            double w = Fat(kv, r, u);
+#pragma unroll
+                            for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wr[m];
+                            Wr[u] = w * il[u];
+                        }
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) {
+                            double acc = Fat(kv, j, NU + r);
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) acc -= Yr[u] * Wu[u][j];
+                            Gr[t][j] = acc;
+                            double acc2 = Fat(kv, r, NU + j);
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) acc2 -= S.Y[kv][u][j] * Wr[u];
+                            Gc[t][j] = acc2;
+                        }
+                    }
+                    STAMP_LAP(6);
+                    double* const pch = &S.bx[0][0];
+                    static_assert((N + 1) * NZ >= N * NX, "chain storage");
+                    double pu[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pu[i] = S.q[N][NU + i];
+                    #pragma unroll
+                    for (int kk = N - 1; kk >= 1; --kk) {  // p_0 is not needed
+                        double pn[RS];
+#pragma unroll
+                        for (int t = 0; t < RS; ++t) {
+                            double a = hr[t];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) a += Gr[t][j] * pu[j];
+                            pn[t] = a;
+                        }
+                        if (k == kk) {
+#pragma unroll
+                            for (int t = 0; t < RS; ++t)
+                                if (rv[t]) pch[kk * NX + rs[t]] = pn[t];
+                        }
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) pu[i] = readlane_d(pn[i / PARTS], kk * PARTS + i % PARTS);
+                    }
+                    __syncthreads();
+                    double pmine[NX];
+                    {
+                        const double* src = (kv + 1 < N) ? pch + (kv + 1) * NX : &S.q[N][NU];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) pmine[i] = src[i];
+                    }
+                    STAMP_LAP(15);
+                    // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
+                    double kf[NU];
+                    {
+                        double yy[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            double acc = y0[u];
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) acc += Wu[u][i] * pmine[i];
+                            yy[u] = acc;
+                        }
+#pragma unroll
+                        for (int u = NU - 1; u >= 0; --u) {
+                            double acc = -yy[u];
+#pragma unroll
+                            for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * kf[m];
+                            kf[u] = acc * il[u];
+                        }
+                    }
+                    double ec[RS];
+#pragma unroll
+                    for (int t = 0; t < RS; ++t) {
+                        double acc = S.rdyn[kv][rs[t]];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) acc += Fat(kv, rs[t], u) * kf[u];
+                        ec[t] = acc;
+                    }
+                    // dx_{kk+1} goes straight to its place in the QP step, ddz[kk + 1]
+                    double dxu[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) dxu[i] = 0.0;
+                    #pragma unroll
+                    for (int kk = 0; kk < N; ++kk) {
+                        double dn[RS];
+#pragma unroll
+                        for (int t = 0; t < RS; ++t) {
+                            double a = ec[t];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) a += Gc[t][j] * dxu[j];
+                            dn[t] = a;
+                        }
+                        if (k == kk) {
+#pragma unroll
+                            for (int t = 0; t < RS; ++t)
+                                if (rv[t]) S.ddz[kk + 1][NU + rs[t]] = dn[t];
+                        }
+                        if (kk + 1 < N) {
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) dxu[i] = readlane_d(dn[i / PARTS], kk * PARTS + i % PARTS);
+                        }
+                    }
+                    __syncthreads();
+                    STAMP_LAP(9);
+                    if (own) {
+                        double dxm[NX], dxn[NX], du[NU];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            dxm[i] = k >= 1 ? S.ddz[k][NU + i] : 0.0;
+                            dxn[i] = S.ddz[k + 1][NU + i];
+                        }
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) du[u] = kf[u];
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) {
+                            double K[NU];
+#pragma unroll
+                            for (int u = NU - 1; u >= 0; --u) {
+                                double acc = -S.Y[k][u][j];
+#pragma unroll
+                                for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * K[m];
+                                K[u] = acc * il[u];
+                            }
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) du[u] += K[u] * dxm[j];
+                        }
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) S.ddz[k][u] = du[u];
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) {
+                            if (k == 0) S.ddz[0][NU + i] = 0.0;
+                            double a = pmine[i];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
+                            S.pin[k][i] = a;
+                        }
+                        if (k == N - 1) {
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) S.ddz[N][u] = 0.0;
+                        }
+                    }
+                } else
                 {
                     const bool own = stage_lane && k < N;
                     const int kq = own ? k : 0;
