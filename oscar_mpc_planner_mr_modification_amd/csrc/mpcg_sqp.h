@@ -174,6 +174,18 @@ struct Lds {
 #define STAMP_STORE(ptr, sol) do {} while (0)
 #endif
 
+// One wavefront per workgroup (blockDim 64): the lanes exchange data through LDS,
+// and a wave's LDS instructions execute in issue order, so an exchange needs a
+// compiler barrier only, not an s_waitcnt on the producing stores before the
+// consuming loads issue (-DMPCG_LDS_WAIT restores __syncthreads for A/B runs).
+__device__ __forceinline__ void wave_sync() {
+#ifdef MPCG_LDS_WAIT
+    __syncthreads();
+#else
+    __asm__ volatile("" ::: "memory");
+#endif
+}
+
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -421,9 +433,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     for (int e = lane; e < N * NX; e += 64)
         (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
     for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
-    __syncthreads();
+    wave_sync();
     if (lane < NU) S.z[N][lane] = 0.0;
-    __syncthreads();
+    wave_sync();
 
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0;
     double res_eq = 0.0;
@@ -562,7 +574,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             res_eq = wave_max(resl);
             if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
         }
-        __syncthreads();
+        wave_sync();
         STAMP_END(0);
 
         // =============== feedback: QP by Riccati interior point ===============
@@ -600,7 +612,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < NX; ++i) S.piq[k][i] = 0.0;
             }
         }
-        __syncthreads();
+        wave_sync();
         STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
         double pinr[C::COMPACT ? NX : 1];  // C::COMPACT: the new dynamics multipliers of the own stage
@@ -668,7 +680,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
                     for (int i = 0; i < NB; ++i) acc[i] += __shfl_down(rh[i], p);
-                __syncthreads();  // the owner lanes' box sums S.bx
+                wave_sync();  // the owner lanes' box sums S.bx
                 if (stage_lane) {
                     double rbox[NZ];
 #pragma unroll
@@ -719,7 +731,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { qstat = AC_NAN; break; }
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
-            __syncthreads();
+            wave_sync();
             STAMP_END(2);
 
             double alpha = 1.0, sigma_mu = 0.0;
@@ -786,7 +798,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int i = 0; i < NBT; ++i) ab[i] += __shfl_down(dbh[i], p);
                         }
                     }
-                    __syncthreads();  // the owner lanes' box sums S.bx
+                    wave_sync();  // the owner lanes' box sums S.bx
                     if (stage_lane) {
 #pragma unroll
                         for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[i] + S.g[k][i] + S.bx[k][i];
@@ -798,7 +810,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                 }
-                __syncthreads();
+                wave_sync();
                 STAMP_END(3);
                 // ---- Riccati factorisation (predictor only; the corrector reuses it)
                 STAMP_BEGIN();
@@ -827,7 +839,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // bicycle instance keeps the LDS flag: there the hoisted reads spill.
                     bool fbad = false;
                     if (C::COMPACT && lane == 0) S.flag = 0;
-                    __syncthreads();
+                    wave_sync();
                     // prefetch of stage N-1's block
                     const int le = lane < NT ? lane : 0;
                     double fi[NX], fj[NX], hv;
@@ -882,7 +894,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             if (lane < NT) S.Msc[lane] = v;
                         }
                         STAMP_LAP(16);
-                        __syncthreads();
+                        wave_sync();
                         STAMP_LAP(17);
                         if constexpr (NU == 2) {
                           if (FAC_FLAT || lane < NP) {
@@ -968,7 +980,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
                         hv = hv2;
                         STAMP_LAP(18);
-                        __syncthreads();
+                        wave_sync();
                         STAMP_LAP(19);
                     }
                     if (C::COMPACT ? S.flag != 0 : __any(fbad)) { qstat = AC_NAN; break; }
@@ -1090,7 +1102,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                         for (int i = 0; i < NX; ++i) pu[i] = readlane_d(pn[i / PARTS], kk * PARTS + i % PARTS);
                     }
-                    __syncthreads();
+                    wave_sync();
                     double pmine[NX];
                     {
                         const double* src = (kv + 1 < N) ? pch + (kv + 1) * NX : &S.q[N][NU];
@@ -1149,7 +1161,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int i = 0; i < NX; ++i) dxu[i] = readlane_d(dn[i / PARTS], kk * PARTS + i % PARTS);
                         }
                     }
-                    __syncthreads();
+                    wave_sync();
                     STAMP_LAP(9);
                     if (own) {
                         double dxm[NX], dxn[NX], du[NU];
@@ -1292,7 +1304,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     if constexpr (CHAIN_REC) {
-                        __syncthreads();
+                        wave_sync();
                         const double* src = (kq + 1 < N) ? pch + (kq + 1) * NX : &S.q[N][NU];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) pmine[i] = src[i];
@@ -1353,7 +1365,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                     if constexpr (CHAIN_REC) {
-                        __syncthreads();
+                        wave_sync();
 #pragma unroll
                         for (int i = 0; i < NX; ++i) dxmine[i] = (k >= 1 && k < N) ? S.ddz[k][NU + i] : 0.0;
                     }
@@ -1401,7 +1413,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                 }
-                __syncthreads();
+                wave_sync();
                 STAMP_END(5);
                 // ---- inequality steps, step length, predictor statistics, row update
                 STAMP_BEGIN();
@@ -1486,7 +1498,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         }
                     }
                 }
-                __syncthreads();
+                wave_sync();
                 STAMP_END(7);
             }
             if (qstat == AC_NAN) break;
@@ -1504,10 +1516,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     }
                 }
             }
-            __syncthreads();
+            wave_sync();
             STAMP_END(8);
         }
-        __syncthreads();
+        wave_sync();
         qp_status = qstat;
         qp_total += qit;
         ++sqp_iter;
@@ -1531,7 +1543,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
         for (int r = 0; r < HS; ++r)
             if (LR.h_on(r)) R.nlam[r] = R.l[HB + r];
-        __syncthreads();
+        wave_sync();
         acados_status = AC_SUCCESS;
         if (qstat != AC_SUCCESS) break;
     }
