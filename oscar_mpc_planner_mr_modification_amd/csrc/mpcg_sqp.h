@@ -112,7 +112,16 @@ struct Cfg {
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // the vector chains split over the parts of a stage (rows of the backward map, columns of
     // the forward one); the register-starved bicycle instance keeps one owner per stage
-    static constexpr bool CHAIN_SPLIT = !COMPACT;
+#ifndef MPCG_C3_SPLIT
+#define MPCG_C3_SPLIT 0
+#endif
+#ifndef MPCG_C3_FACFLAT
+#define MPCG_C3_FACFLAT 0
+#endif
+    static constexpr bool CHAIN_SPLIT = !COMPACT || MPCG_C3_SPLIT;
+    // branch-free Riccati step (every lane, prefetch after the pivot reads, pivot failures
+    // voted from a register)
+    static constexpr bool FAC_FLAT = !COMPACT || MPCG_C3_FACFLAT;
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -816,7 +825,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 STAMP_BEGIN();
                 if (phase == 0) {
                     constexpr int NT = C::NTRI, NP = C::NPT, DZ = C::NDH - 1;
-                    constexpr bool FAC_FLAT = !C::COMPACT;
+                    constexpr bool FAC_FLAT = C::FAC_FLAT;
                     // element lane -> (ei, ej), ei >= ej, of the nz x nz block
                     int ei = 0;
                     while ((ei + 1) * (ei + 2) / 2 <= lane && ei < NZ - 1) ++ei;
@@ -838,7 +847,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // scheduler from hoisting the next LDS reads over it).  The register-starved
                     // bicycle instance keeps the LDS flag: there the hoisted reads spill.
                     bool fbad = false;
-                    if (C::COMPACT && lane == 0) S.flag = 0;
+                    if (!FAC_FLAT && lane == 0) S.flag = 0;
                     wave_sync();
                     // prefetch of stage N-1's block
                     const int le = lane < NT ? lane : 0;
@@ -862,7 +871,6 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         // products advance together, and the prefetch is issued after the pivot
                         // block's reads (off the recursion's critical path, and not in front of
                         // the LDS traffic the next step waits for)
-                        static_assert(!FAC_FLAT || NU == 2, "flat factorisation: 2 inputs");
                         const int kn = kk > 0 ? kk - 1 : 0;
                         double fi2[NX], fj2[NX], hv2;
                         auto prefetch = [&]() {
@@ -925,13 +933,28 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             if (pj_ == 0 && lane < NP) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
                             if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
                           }
-                        } else if (lane < NP) {
+                        } else if (FAC_FLAT || lane < NP) {
                             // Cholesky of Muu through reciprocal square roots
                             double Lm[NU][NU], il[NU];
                             bool bad = false;
+                            double Mu[C::NTRI > 0 ? NU * (NU + 1) / 2 : 1], Mi[NU], Mj[NU], mij = 0.0;
+                            if constexpr (FAC_FLAT) {
+#pragma unroll
+                                for (int e = 0; e < NU * (NU + 1) / 2; ++e) Mu[e] = S.Msc[e];
+#pragma unroll
+                                for (int u = 0; u < NU; ++u) { Mi[u] = S.Msc[sym(NU + pi_, u)]; Mj[u] = S.Msc[sym(NU + pj_, u)]; }
+                                mij = S.Msc[sym(NU + pi_, NU + pj_)];
+                                __builtin_amdgcn_sched_barrier(0);
+                                prefetch();
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                            auto msc = [&](int i, int j) -> double {  // entry of the pivot block
+                                if constexpr (FAC_FLAT) return Mu[sym(i, j)];
+                                else return S.Msc[sym(i, j)];
+                            };
 #pragma unroll
                             for (int j = 0; j < NU; ++j) {
-                                double d = S.Msc[sym(j, j)];
+                                double d = msc(j, j);
 #pragma unroll
                                 for (int m = 0; m < j; ++m) d -= Lm[j][m] * Lm[j][m];
                                 il[j] = frsq(d);
@@ -939,31 +962,32 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                                 bad = bad || !(d > 0.0);
 #pragma unroll
                                 for (int i = j + 1; i < NU; ++i) {
-                                    double acc = S.Msc[sym(i, j)];
+                                    double acc = msc(i, j);
 #pragma unroll
                                     for (int m = 0; m < j; ++m) acc -= Lm[i][m] * Lm[j][m];
                                     Lm[i][j] = acc * il[j];
                                 }
                             }
-                            if constexpr (C::COMPACT) {
-                                if (bad) S.flag = 1;
-                            } else {
+                            if constexpr (FAC_FLAT) {
                                 fbad = fbad | bad;
+                            } else {
+                                if (bad) S.flag = 1;
                             }
                             double yi[NU], yj[NU];
 #pragma unroll
                             for (int u = 0; u < NU; ++u) {
-                                double ai = S.Msc[sym(NU + pi_, u)], aj = S.Msc[sym(NU + pj_, u)];
+                                double ai = FAC_FLAT ? Mi[u] : S.Msc[sym(NU + pi_, u)];
+                                double aj = FAC_FLAT ? Mj[u] : S.Msc[sym(NU + pj_, u)];
 #pragma unroll
                                 for (int m = 0; m < u; ++m) { ai -= Lm[u][m] * yi[m]; aj -= Lm[u][m] * yj[m]; }
                                 yi[u] = ai * il[u];
                                 yj[u] = aj * il[u];
                             }
-                            double pv = S.Msc[sym(NU + pi_, NU + pj_)];
+                            double pv = FAC_FLAT ? mij : S.Msc[sym(NU + pi_, NU + pj_)];
 #pragma unroll
                             for (int u = 0; u < NU; ++u) pv -= yi[u] * yj[u];
-                            S.P[kk][lane] = pv;
-                            if (pj_ == 0) {
+                            *(lane < NP ? &S.P[kk][lane] : &S.Msc[64 + lane]) = pv;
+                            if (pj_ == 0 && lane < NP) {
 #pragma unroll
                                 for (int u = 0; u < NU; ++u) S.Y[kk][u][pi_] = yi[u];
                             }
@@ -983,13 +1007,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         wave_sync();
                         STAMP_LAP(19);
                     }
-                    if (C::COMPACT ? S.flag != 0 : __any(fbad)) { qstat = AC_NAN; break; }
+                    if (FAC_FLAT ? __any(fbad) : S.flag != 0) { qstat = AC_NAN; break; }
                 }
                 STAMP_END(4);
                 // ---- vector + forward passes: affine 5-vector recursions in SGPRs
                 STAMP_BEGIN();
                 if constexpr (C::CHAIN_SPLIT) {
-                    static_assert(NU == 2, "split chains: 2 inputs");
                     // Every part of stage k owns the rows {part + PARTS s} of the stage's
                     // backward map p_k = h_k + G_k p_{k+1} and the same columns of the forward
                     // map dx_{k+1} = G_k' dx_k + e_k: a chain step is RS short dot products per
@@ -1000,7 +1023,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     const int kv = k < N ? k : 0;
                     const bool own = stage_lane && k < N;
                     double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
-                    Lo[0] = S.Lc[kv][1]; il[0] = S.Lc[kv][2]; il[1] = S.Lc[kv][3];
+                    if constexpr (NU == 2) {
+                        Lo[0] = S.Lc[kv][1]; il[0] = S.Lc[kv][2]; il[1] = S.Lc[kv][3];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kv][i];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) il[u] = S.Lc[kv][C::NLO + u];
+                    }
+                    // dynamics residual of stage kv (C::COMPACT recomputes it)
+                    auto rdyn_v = [&](int i) -> double {
+                        if constexpr (C::COMPACT) return rdyn_at(kv, i);
+                        else return S.rdyn[kv][i];
+                    };
                     int rs[RS];
                     bool rv[RS];
 #pragma unroll
@@ -1012,7 +1047,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     {
                         double rr[NX];
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) rr[i] = S.rdyn[kv][i];
+                        for (int i = 0; i < NX; ++i) rr[i] = rdyn_v(i);
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             double a = 0.0;
@@ -1132,7 +1167,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double ec[RS];
 #pragma unroll
                     for (int t = 0; t < RS; ++t) {
-                        double acc = S.rdyn[kv][rs[t]];
+                        double acc = rdyn_v(rs[t]);
 #pragma unroll
                         for (int u = 0; u < NU; ++u) acc += Fat(kv, rs[t], u) * kf[u];
                         ec[t] = acc;
@@ -1193,7 +1228,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            S.pin[k][i] = a;
+                            if constexpr (C::COMPACT) pinr[i] = a;
+                            else S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
 #pragma unroll
