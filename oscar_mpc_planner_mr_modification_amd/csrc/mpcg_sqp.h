@@ -906,7 +906,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         STAMP_LAP(17);
                         if constexpr (NU == 2) {
                           if (FAC_FLAT || lane < NP) {
-                            const double m00 = S.Msc[0], m10 = S.Msc[1], m11 = S.Msc[2];
+                            // the pivot block (element lanes 0, 1, 2) straight from their registers:
+                            // the recursion's critical path skips one LDS round trip
+                            const double m00 = FAC_FLAT ? readlane_d(v, 0) : S.Msc[0];
+                            const double m10 = FAC_FLAT ? readlane_d(v, 1) : S.Msc[1];
+                            const double m11 = FAC_FLAT ? readlane_d(v, 2) : S.Msc[2];
                             const double mi0 = S.Msc[sym(NU + pi_, 0)], mi1 = S.Msc[sym(NU + pi_, 1)];
                             const double mj0 = S.Msc[sym(NU + pj_, 0)], mj1 = S.Msc[sym(NU + pj_, 1)];
                             const double mij = S.Msc[sym(NU + pi_, NU + pj_)];
