@@ -122,6 +122,9 @@ struct Cfg {
     // branch-free Riccati step (every lane, prefetch after the pivot reads, pivot failures
     // voted from a register)
     static constexpr bool FAC_FLAT = !COMPACT || MPCG_C3_FACFLAT;
+    // branch-free chain records (three parts per stage: C2 13.40 -> 12.92 ms, C5 23.45 -> 22.75;
+    // the two-part long horizon C4 spills with it, 56.4 -> 76.2 ms)
+    static constexpr bool REC_FLAT = CHAIN_SPLIT && PARTS == 3;
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -1133,7 +1136,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += Gr[t][j] * pu[j];
                             pn[t] = a;
                         }
-                        if (k == kk) {
+                        if constexpr (C::REC_FLAT) {
+                            // branch-free record: lanes that do not own the step write to the
+                            // dead pivot scratch (the stores then sink below the broadcast)
+#pragma unroll
+                            for (int t = 0; t < RS; ++t)
+                                *((k == kk && rv[t]) ? &pch[kk * NX + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = pn[t];
+                        } else if (k == kk) {
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
                                 if (rv[t]) pch[kk * NX + rs[t]] = pn[t];
@@ -1190,7 +1199,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int j = 0; j < NX; ++j) a += Gc[t][j] * dxu[j];
                             dn[t] = a;
                         }
-                        if (k == kk) {
+                        if constexpr (C::REC_FLAT) {
+#pragma unroll
+                            for (int t = 0; t < RS; ++t)
+                                *((k == kk && rv[t]) ? &S.ddz[kk + 1][NU + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = dn[t];
+                        } else if (k == kk) {
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
                                 if (rv[t]) S.ddz[kk + 1][NU + rs[t]] = dn[t];
