@@ -88,6 +88,7 @@ static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG
 
 template <class C>
 static int launch(const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream) {
+    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync)
     hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, stream, pr, batch, io, g_stamps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
