@@ -203,15 +203,40 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
     return __hiloint2double(hi, lo);
 }
+// DPP move of both halves of a double (lanes outside row_mask keep `v`)
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), CTRL, ROW_MASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, ROW_MASK, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_max(double v) {
+#ifdef MPCG_MAX_BPERMUTE
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
+#else
+    // max is exact in any order: a DPP tree (quads, half rows, rows, then row 15 /
+    // row 31 broadcasts) instead of six ds_bpermute levels, lane 63 broadcast
+    v = fmax(v, dpp_d<0xB1>(v));        // quad_perm [1,0,3,2]
+    v = fmax(v, dpp_d<0x4E>(v));        // quad_perm [2,3,0,1]
+    v = fmax(v, dpp_d<0x141>(v));       // row_half_mirror
+    v = fmax(v, dpp_d<0x140>(v));       // row_mirror
+    v = fmax(v, dpp_d<0x142, 0xA>(v));  // row_bcast15 -> rows 1, 3
+    v = fmax(v, dpp_d<0x143, 0xC>(v));  // row_bcast31 -> rows 2, 3
+    return readlane_d(v, 63);
+#endif
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    // the same DPP tree as wave_max: every lane gets lane 63's sum, so the result is
+    // bit-identical across lanes and deterministic (one fixed association order)
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    v += dpp_d<0x142, 0xA>(v);
+    v += dpp_d<0x143, 0xC>(v);
+    return readlane_d(v, 63);
 }
 
 
