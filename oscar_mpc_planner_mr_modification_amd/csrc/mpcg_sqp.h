@@ -210,6 +210,17 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, ROW_MASK, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+// value of lane + p (p = 1, 2: the other parts of a stage) for part 0's fold: DPP
+// whole-wave shifts (wave_shl:1) instead of ds_bpermute (-DMPCG_FOLD_BPERMUTE restores it)
+__device__ __forceinline__ double lane_down(double v, int p) {
+#ifdef MPCG_FOLD_BPERMUTE
+    return __shfl_down(v, p);
+#else
+    double w = dpp_d<0x130>(v);
+    if (p == 2) w = dpp_d<0x130>(w);
+    return w;
+#endif
+}
 __device__ __forceinline__ double wave_max(double v) {
 #ifdef MPCG_MAX_BPERMUTE
 #pragma unroll
@@ -498,7 +509,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) acc[i] += __shfl_down(hb6[i], p);
+                    for (int i = 0; i < 6; ++i) acc[i] += lane_down(hb6[i], p);
 #pragma unroll
                 for (int i = 0; i < 6; ++i) hb6[i] = acc[i];
             }
@@ -716,7 +727,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                 for (int p = 1; p < PARTS; ++p)
 #pragma unroll
-                    for (int i = 0; i < NB; ++i) acc[i] += __shfl_down(rh[i], p);
+                    for (int i = 0; i < NB; ++i) acc[i] += lane_down(rh[i], p);
                 wave_sync();  // the owner lanes' box sums S.bx
                 if (stage_lane) {
                     double rbox[NZ];
@@ -829,10 +840,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                     for (int p = 1; p < PARTS; ++p) {
 #pragma unroll
-                        for (int i = 0; i < NB; ++i) aq[i] += __shfl_down(qh[i], p);
+                        for (int i = 0; i < NB; ++i) aq[i] += lane_down(qh[i], p);
                         if (phase == 0) {
 #pragma unroll
-                            for (int i = 0; i < NBT; ++i) ab[i] += __shfl_down(dbh[i], p);
+                            for (int i = 0; i < NBT; ++i) ab[i] += lane_down(dbh[i], p);
                         }
                     }
                     wave_sync();  // the owner lanes' box sums S.bx
