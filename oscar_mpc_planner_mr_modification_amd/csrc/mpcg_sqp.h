@@ -198,6 +198,18 @@ __device__ __forceinline__ void wave_sync() {
 #endif
 }
 
+#ifndef MPCG_REC_SELECT
+typedef __attribute__((address_space(3))) double lds_double;
+// lanes in MASK get `on`, the others `off` (a literal lane mask: no per-step compare and no
+// precomputed per-step addresses kept in registers)
+__device__ __forceinline__ unsigned sel_lanes(unsigned long long mask, unsigned off, unsigned on) {
+    unsigned r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(off), "v"(on), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ unsigned lds_addr(double* p) { return (unsigned)(size_t)(lds_double*)p; }
+__device__ __forceinline__ void lds_store(unsigned a, double v) { *(lds_double*)(size_t)a = v; }
+#endif
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -1175,9 +1187,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         if constexpr (C::REC_FLAT) {
                             // branch-free record: lanes that do not own the step write to the
                             // dead pivot scratch (the stores then sink below the broadcast)
+#ifndef MPCG_REC_SELECT
+                            // owner lanes of step kk: the literal mask of stage kk's parts; both
+                            // candidate addresses are lane constants offset by the step's stride
+                            const unsigned long long OWN = ((1ull << PARTS) - 1) << (kk * PARTS);
+                            static_assert((N - 1) * NX + 8 <= 128, "record dummies inside the pivot scratch");
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                const unsigned on = rv[t] ? lds_addr(&pch[rs[t]]) : lds_addr(&S.Msc[lane & 7]);
+                                const unsigned off = lds_addr(&S.Msc[lane & 7]);
+                                lds_store(sel_lanes(OWN, off, on) + kk * NX * 8, pn[t]);
+                            }
+#else
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
                                 *((k == kk && rv[t]) ? &pch[kk * NX + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = pn[t];
+#endif
                         } else if (k == kk) {
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
@@ -1236,9 +1261,21 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             dn[t] = a;
                         }
                         if constexpr (C::REC_FLAT) {
+#ifndef MPCG_REC_SELECT
+                            // dummies in the box-sum rows (the backward chain's values are read)
+                            const unsigned long long OWN = ((1ull << PARTS) - 1) << (kk * PARTS);
+                            static_assert((N - 1) * NZ + 8 <= (N + 1) * NZ, "record dummies inside the box-sum rows");
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                const unsigned off = lds_addr(&S.bx[0][lane & 7]);
+                                const unsigned on = rv[t] ? lds_addr(&S.ddz[1][NU + rs[t]]) : off;
+                                lds_store(sel_lanes(OWN, off, on) + kk * NZ * 8, dn[t]);
+                            }
+#else
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
                                 *((k == kk && rv[t]) ? &S.ddz[kk + 1][NU + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = dn[t];
+#endif
                         } else if (k == kk) {
 #pragma unroll
                             for (int t = 0; t < RS; ++t)
