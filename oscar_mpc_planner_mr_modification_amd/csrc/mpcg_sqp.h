@@ -122,9 +122,16 @@ struct Cfg {
     // branch-free Riccati step (every lane, prefetch after the pivot reads, pivot failures
     // voted from a register)
     static constexpr bool FAC_FLAT = !COMPACT || MPCG_C3_FACFLAT;
+#ifndef MPCG_REC_P2
+#define MPCG_REC_P2 0
+#endif
     // branch-free chain records (three parts per stage: C2 13.40 -> 12.92 ms, C5 23.45 -> 22.75;
     // the two-part long horizon C4 spills with it, 56.4 -> 76.2 ms)
+#ifdef MPCG_REC_SELECT
     static constexpr bool REC_FLAT = CHAIN_SPLIT && PARTS == 3;
+#else
+    static constexpr bool REC_FLAT = CHAIN_SPLIT && (PARTS == 3 || MPCG_REC_P2);
+#endif
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -1191,11 +1198,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             // owner lanes of step kk: the literal mask of stage kk's parts; both
                             // candidate addresses are lane constants offset by the step's stride
                             const unsigned long long OWN = ((1ull << PARTS) - 1) << (kk * PARTS);
-                            static_assert((N - 1) * NX + 8 <= 128, "record dummies inside the pivot scratch");
+                            // dummies in the QP step rows (dead until the forward chain writes them)
+                            static_assert((N - 1) * NX + 8 <= (N + 1) * NZ, "record dummies inside the QP step rows");
 #pragma unroll
                             for (int t = 0; t < RS; ++t) {
-                                const unsigned on = rv[t] ? lds_addr(&pch[rs[t]]) : lds_addr(&S.Msc[lane & 7]);
-                                const unsigned off = lds_addr(&S.Msc[lane & 7]);
+                                const unsigned off = lds_addr(&S.ddz[0][lane & 7]);
+                                const unsigned on = rv[t] ? lds_addr(&pch[rs[t]]) : off;
                                 lds_store(sel_lanes(OWN, off, on) + kk * NX * 8, pn[t]);
                             }
 #else
