@@ -62,6 +62,14 @@ struct Cfg {
     static constexpr int NH = NL + NE + NS;
     static constexpr int NTRI = NZ * (NZ + 1) / 2;  // packed stage block
     static constexpr int NPT = NX * (NX + 1) / 2;   // packed cost-to-go
+#ifndef MPCG_P_PAD
+#define MPCG_P_PAD 1
+#endif
+    // cost-to-go rows padded to an even count of doubles: every stage's broadcast read is
+    // 16-B aligned (ds_read_b128 with immediate offsets instead of ds_read2_b64 on every
+    // other stage): C2 12.49 -> 12.26 ms, C5 20.51 -> 19.93.  Not on the long horizons
+    // (C4 measured 53.84 -> 54.19) nor on the compact C3 storage (at its occupancy line)
+    static constexpr int NPTP = (MPCG_P_PAD && MODEL_ != 1 && (64 / (N_ + 1)) >= 3) ? NPT + (NPT & 1) : NPT;
     // h rows touch (x, y, psi) and, with the slack model, the slack state:
     // the barrier block of the h rows is NB x NB on those variables
     static constexpr int NB = (HAS_SLACK && NS > 0) ? 4 : 3;
@@ -152,7 +160,7 @@ struct Lds {
     double piq[N][NX];
     double pin[C::COMPACT ? 1 : N][NX];
     double rdyn[C::COMPACT ? 1 : N][NX];
-    double P[N + 1][C::NPT];  // Riccati cost-to-go, packed
+    alignas(16) double P[N + 1][C::NPTP];  // Riccati cost-to-go, packed (row padded, C::NPTP)
     double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane;
