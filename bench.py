@@ -3,34 +3,38 @@
 
 Workload (BASELINE.json configs[1], "C2"): jackal unicycle T-MPC++, N=20,
 8 obstacles, 1024 synthetic scenes x 8 topology guesses per GPU (7 guided +
-the non-guided T-MPC++ planner), 10 SQP-RTI iterations per solve, timeout
-disabled.  One step = one control step of every scene, all on the GPU:
-per-guess solver inputs from the scene data (mpcg_prepare: warm starts,
-topology halfspaces with Douglas-Rachford projection, obstacles, consistency
-references) + one batched solve of all scenes x guesses + per-scene planner
-selection (FindBestPlanner with the consistency and selection-weight
-bookkeeping) + one RCCL all-gather of the winning trajectories when
-N_gpus > 1 (scenes are sharded, weak scaling).  Scene data is uploaded once
-before the timed region (inputs resident in HBM).
+the non-guided T-MPC++ planner), up to 10 SQP-RTI iterations per solve (the
+reference's loop breaks on a failed QP; `solver_stats.rti_iters_per_solve` is
+the executed count), timeout disabled.  One step = one control step of every
+scene, all on the GPU: per-guess solver inputs from the scene data
+(mpcg_prepare: warm starts, topology halfspaces with Douglas-Rachford
+projection, obstacles, consistency references) + one batched solve of all
+scenes x guesses + per-scene planner selection (FindBestPlanner with the
+consistency and selection-weight bookkeeping) + one RCCL all-gather of the
+winning trajectories when N_gpus > 1 (scenes are sharded, weak scaling).
+Scene data is uploaded once before the timed region (inputs resident in HBM).
 
-    python bench.py [--gpus N --steps K --warmup W]
-    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+    python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C4|C5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  `roofline` prices the solve kernel against HBM
 with SURVEY.md §8(d)'s algorithmic bytes per solve (the path is fp64-VALU /
-latency bound); `cpu_baseline` times the C oracle (same
-algorithm, OpenMP over solves) on a bounded sample of the same batch, and
-`parity` is max |x - x_ref| over that sample.
+latency bound); `roofline.traffic` comes from the rocprofv3 PMC
+summary under profiles/ only when that summary was taken on the same kernel
+sources (source hash), else it is null.  `cpu_baseline` times the C oracle
+(same algorithm, OpenMP over solves) on a bounded sample of the same batch
+(rank 0, N=1), and `parity` is the oracle check of that sample; at N>1 every
+rank checks a sample of its own shard and the results are reduced over ranks.
 
-`--config C3` runs the curvature-aware bicycle workload:
-4096 scenes per GPU, N=30, the bicycle with the CA spline update, CA
-contouring and 12 decomp halfspaces per stage, one solver per scene.
-
-`--config C5` runs the SH-MPC workload instead: 2048
-scenes x 4 parallel scenario solvers per GPU on the slack model, 24 scenario
-halfspaces per stage reduced on the GPU from 12 obstacles x 100 prediction
-samples (mpcg_prepare_scenario), batched solve, lowest-cost pick
-(ScenarioConstraints::optimize) and the winner gather.
+`--config C3`: the curvature-aware bicycle workload, 4096
+scenes per GPU, N=30, CA spline update, CA contouring and 12 decomp
+halfspaces per stage, one solver per scene.
+`--config C4`: N=30, 12 obstacles, 2048 scenes x 8 guesses per GPU (one GPU's
+shard of BASELINE.json configs[3]).
+`--config C5`: SH-MPC, 2048 scenes x 4 parallel scenario solvers per GPU on the
+slack model, 24 scenario halfspaces per stage reduced on the GPU from 12
+obstacles x 100 prediction samples (mpcg_prepare_scenario), batched solve,
+lowest-cost pick (ScenarioConstraints::optimize) and the winner gather.
 """
 import argparse
 import json
@@ -46,6 +50,9 @@ sys.path.insert(0, ROOT)
 METRIC = "SQP solves/s (N=20, 8 obs, 8 guesses) at 1/2/4/8 MI355X; max |x−x_ref|"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (vendor spec)
+DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048}
+CHECK_CHUNK = 256              # solves per oracle call in the check leg
+RANK_SAMPLE = 256              # solves each rank checks at N > 1
 
 
 def algorithmic_bytes_per_solve(lay):
@@ -54,25 +61,309 @@ def algorithmic_bytes_per_solve(lay):
     return 8 * (N * lay.npar + (N + 1) * lay.nvar + lay.nx + (N + 1) * lay.nx + N * lay.nu + 2)
 
 
+def load_counters(path, config, batch):
+    """PMC summary (scripts/summarize_profile.py) of the solve kernel, used only when it
+    was collected on the same kernel sources and batch: returns (traffic, fp64, note)."""
+    from oscar_mpc_planner_mr_modification_amd._build import source_hash
+
+    if not os.path.exists(path):
+        return None, None, "no PMC summary"
+    try:
+        tj = json.load(open(path))
+    except Exception as e:  # noqa: BLE001
+        return None, None, f"unreadable PMC summary: {e}"
+    if tj.get("config") != config or tj.get("batch") != batch:
+        return None, None, f"PMC summary {tj.get('tag')} is for {tj.get('config')} batch {tj.get('batch')}"
+    if tj.get("source_sha256") != source_hash():
+        return None, None, f"PMC summary {tj.get('tag')} was taken on other kernel sources (stale)"
+    return tj.get("hbm_bytes_per_launch"), tj.get("fp64_issued_flop_per_launch"), f"profiles/{tj.get('tag')}"
+
+
+# ----------------------------------------------------------------- workloads
+class Workload:
+    """One config's GPU step: `step(timed)` enqueues one control step of every scene
+    on `stream`; phase events are recorded when timed."""
+    phases = ("solve",)
+
+    def __init__(self, args, lay, rank, world, dev):
+        self.args, self.lay, self.rank, self.world, self.dev = args, lay, rank, world, dev
+        self.S = args.scenes or DEFAULT_SCENES[args.config]
+        self.threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+    def host_inputs(self, lo, hi):
+        """host copies (params, warm, xinit) of solves [lo, hi) for the oracle check"""
+        raise NotImplementedError
+
+    def gather(self, winners):
+        from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners
+        if self.world > 1:
+            gather_winners(winners, self.world, out=self.gathered)
+
+
+class TmpcWorkload(Workload):
+    """C1 / C2 / C4: T-MPC++ control step (prepare -> solve -> select -> winner records)."""
+    phases = ("prepare", "solve")
+
+    def __init__(self, args, lay, rank, world, dev):
+        super().__init__(args, lay, rank, world, dev)
+        import torch
+
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_width
+        from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+        S, G, N = self.S, args.guesses, lay.N
+        self.G, self.B = G, S * G
+        t0 = time.time()
+        self.batch = make_batch(lay, S, G, first_scene=rank * S, workers=min(self.threads, 16))
+        self.gen_s = time.time() - t0
+        self.scenes = self.batch.scenes
+        self.dsc = native.scenes_to_device(self.scenes, dev)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        B = self.B
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, 7), **f64),
+                         xinit=torch.empty((B, 5), **f64), prev_interp=torch.empty((S, N, 2), **f64),
+                         consistency_active=torch.empty((B,), dtype=torch.uint8, device=dev))
+        self.out = dict(xtraj=torch.empty((B, N + 1, 5), **f64), utraj=torch.empty((B, N, 2), **f64),
+                        pobj=torch.empty((B,), **f64), exit=torch.empty((B,), dtype=torch.int32, device=dev),
+                        info=torch.empty((B, 4), dtype=torch.int32, device=dev))
+        self.winners = torch.empty((S, winner_width(N)), **f64)
+        self.gathered = torch.empty((S * world, winner_width(N)), **f64) if world > 1 else None
+        self.workload = (f"{args.config}: jackal unicycle T-MPC++, N={N}, {lay.max_obstacles} obstacles, {S} scenes x "
+                         f"{G} guesses per GPU, up to {lay.sqp_iters} SQP-RTI iterations per solve")
+        self.config = {"scenes_per_gpu": S, "guesses": G, "N": N, "obstacles": lay.max_obstacles}
+
+    def step(self, ev=None):
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
+        from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION, ROBOT_RADIUS, SETTINGS_WEIGHTS
+
+        s = self.stream
+        if ev:
+            ev[0].record(s)
+        native.prepare_device(self.pr, self.dsc, ROBOT_RADIUS, SETTINGS_WEIGHTS["consistency"], DECELERATION,
+                              out=self.prep, stream=s)
+        if ev:
+            ev[1].record(s)
+        native.solve_batch_device(self.pr, self.prep["params"], self.prep["warm"], self.prep["xinit"], out=self.out,
+                                  stream=s)
+        if ev:
+            ev[2].record(s)
+        best, _ = native.select_best_device(self.S, self.G, self.lay.N, self.out["xtraj"], self.out["pobj"],
+                                            self.out["exit"], prev_traj=self.prep["prev_interp"],
+                                            w_cons=SETTINGS_WEIGHTS["consistency"],
+                                            consistency_enabled=self.prep["consistency_active"],
+                                            previously_selected=self.dsc["previously_selected"],
+                                            selection_weight=0.75, stream=s)   # guidance_planner.yaml:37
+        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, self.G, out=self.winners)
+        self.gather(self.winners)
+
+    def host_inputs(self, lo, hi):
+        # the GPU producer is bit-identical to the host restatement (tests/test_producers.py)
+        b = self.batch
+        return b.params[lo:hi], b.warm[lo:hi], b.xinit[lo:hi]
+
+
+class C3Workload(Workload):
+    """C3: one batched solve of every scene's bicycle CA-MPC problem + the result gather
+    (the decomp halfspaces come from DecompUtil, external, so the per-scene solver inputs
+    are built on the host once, resident in HBM before the timed region)."""
+
+    def __init__(self, args, lay, rank, world, dev):
+        super().__init__(args, lay, rank, world, dev)
+        import torch
+
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_width
+
+        S, N, nx, nu = self.S, lay.N, lay.nx, lay.nu
+        self.B = S
+        t0 = time.time()
+        self.b = make_c3_batch(lay, S, first_scene=rank * S)
+        self.gen_s = time.time() - t0
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.d_par, self.d_warm, self.d_xi = t(self.b.params), t(self.b.warm), t(self.b.xinit)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.out = dict(xtraj=torch.empty((S, N + 1, nx), **f64), utraj=torch.empty((S, N, nu), **f64),
+                        pobj=torch.empty((S,), **f64), exit=torch.empty((S,), dtype=torch.int32, device=dev),
+                        info=torch.empty((S, 4), dtype=torch.int32, device=dev))
+        self.winners = torch.empty((S, winner_width(N, nx, nu)), **f64)
+        self.gathered = torch.empty((S * world, winner_width(N, nx, nu)), **f64) if world > 1 else None
+        self.workload = (f"C3: BicycleModel2ndOrderCurvatureAware + CA-MPC contouring + {lay.n_scen} decomp "
+                         f"halfspaces, N={N}, {S} scenes per GPU, up to {lay.sqp_iters} SQP-RTI iterations per solve")
+        self.config = {"scenes_per_gpu": S, "N": N}
+
+    def step(self, ev=None):
+        import torch
+
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
+
+        s = self.stream
+        if ev:
+            ev[0].record(s)
+        native.solve_batch_device(self.pr, self.d_par, self.d_warm, self.d_xi, out=self.out, stream=s)
+        if ev:
+            ev[1].record(s)
+        best = torch.where(self.out["exit"] == 1, 0, -1).to(torch.int32)
+        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, 1, out=self.winners)
+        self.gather(self.winners)
+
+    def host_inputs(self, lo, hi):
+        b = self.b
+        return b.params[lo:hi], b.warm[lo:hi], b.xinit[lo:hi]
+
+
+class ShmpcWorkload(Workload):
+    """C5: SH-MPC step = scenario producer (samples -> halfspaces) + solve + lowest-cost pick + gather."""
+    phases = ("prepare", "solve")
+
+    def __init__(self, args, lay, rank, world, dev):
+        super().__init__(args, lay, rank, world, dev)
+        import torch
+
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_width
+        from oscar_mpc_planner_mr_modification_amd.scenario import (OBSTACLE_RADIUS, PARALLEL_SOLVERS, ROBOT_RADIUS,
+                                                                    ScenarioScenes, make_shmpc_scenes)
+
+        S, P, N, nx = self.S, PARALLEL_SOLVERS, lay.N, lay.nx
+        self.P, self.B = P, S * P
+        self.n_obs, self.n_samples = 12, 100
+        self.radius = ROBOT_RADIUS + OBSTACLE_RADIUS
+        t0 = time.time()
+        workers, first = min(self.threads, 16), rank * S
+        if workers > 1 and S >= 2 * workers:
+            from concurrent.futures import ProcessPoolExecutor
+            chunks = [c for c in np.array_split(np.arange(S), workers) if len(c)]
+            with ProcessPoolExecutor(max_workers=workers) as ex:
+                parts = list(ex.map(make_shmpc_scenes, [lay] * len(chunks), [len(c) for c in chunks],
+                                    [P] * len(chunks), [self.n_obs] * len(chunks), [self.n_samples] * len(chunks),
+                                    [20251212] * len(chunks), [first + int(c[0]) for c in chunks]))
+            self.scenes = ScenarioScenes(stage_params=np.concatenate([q.stage_params for q in parts]),
+                                         state=np.concatenate([q.state for q in parts]),
+                                         samples=np.concatenate([q.samples for q in parts]), n_solvers=P)
+            del parts
+        else:
+            self.scenes = make_shmpc_scenes(lay, S, P, self.n_obs, self.n_samples, first_scene=first)
+        self.gen_s = time.time() - t0
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.d_sp, self.d_st, self.d_smp = t(self.scenes.stage_params), t(self.scenes.state), t(self.scenes.samples)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        B = self.B
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, lay.nvar), **f64),
+                         xinit=torch.empty((B, nx), **f64))
+        self.out = dict(xtraj=torch.empty((B, N + 1, nx), **f64), utraj=torch.empty((B, N, 2), **f64),
+                        pobj=torch.empty((B,), **f64), exit=torch.empty((B,), dtype=torch.int32, device=dev),
+                        info=torch.empty((B, 4), dtype=torch.int32, device=dev))
+        self.best = torch.empty((S,), dtype=torch.int32, device=dev)
+        self.winners = torch.empty((S, winner_width(N, nx)), **f64)
+        self.gathered = torch.empty((S * world, winner_width(N, nx)), **f64) if world > 1 else None
+        self.workload = (f"C5: SH-MPC slack model, N={N}, {lay.n_scen} scenario halfspaces per stage from "
+                         f"{self.n_obs} obstacles x {self.n_samples} samples, {S} scenes x {P} parallel solvers "
+                         f"per GPU, up to {lay.sqp_iters} SQP-RTI iterations per solve")
+        self.config = {"scenes_per_gpu": S, "parallel_solvers": P, "N": N}
+        self._host = None
+
+    def step(self, ev=None):
+        from oscar_mpc_planner_mr_modification_amd import native
+        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
+        from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION
+
+        s = self.stream
+        if ev:
+            ev[0].record(s)
+        native.prepare_scenario_device(self.pr, self.P, self.d_sp, self.d_st, self.d_smp, self.radius, DECELERATION,
+                                       out=self.prep, stream=s)
+        if ev:
+            ev[1].record(s)
+        native.solve_batch_device(self.pr, self.prep["params"], self.prep["warm"], self.prep["xinit"], out=self.out,
+                                  stream=s)
+        if ev:
+            ev[2].record(s)
+        native.select_lowest_cost_device(self.S, self.P, self.out["pobj"], self.out["exit"], out=self.best, stream=s)
+        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], self.best, self.P, out=self.winners)
+        self.gather(self.winners)
+
+    def host_inputs(self, lo, hi):
+        # the oracle solves the GPU producer's inputs, so parity isolates the solve; the
+        # producer itself is checked against the host restatement on the first scenes
+        if self._host is None:
+            self._host = {k: v.cpu().numpy() for k, v in self.prep.items()}
+        h = self._host
+        return h["params"][lo:hi], h["warm"][lo:hi], h["xinit"][lo:hi]
+
+    def producer_check(self, n_scenes=64):
+        from oscar_mpc_planner_mr_modification_amd.scenario import ScenarioScenes, prepare_scenario_host
+        from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION
+
+        n = min(n_scenes, self.S)
+        sub = ScenarioScenes(stage_params=self.scenes.stage_params[:n], state=self.scenes.state[:n],
+                             samples=self.scenes.samples[:n * self.P], n_solvers=self.P)
+        hb = prepare_scenario_host(self.lay, sub, self.radius, DECELERATION)
+        prm, wrm, _ = self.host_inputs(0, n * self.P)
+        return max(float(np.abs(hb.params - prm).max()), float(np.abs(hb.warm - wrm).max()))
+
+    def producer_roofline(self, prep_ms):
+        lay, N = self.lay, self.lay.N
+        # the producer reads every sample once and streams the solver inputs out
+        prep_bytes = self.B * ((N - 1) * self.n_obs * self.n_samples * 16 + N * lay.npar * 8 + (N + 1) * lay.nvar * 8)
+        gbs = prep_bytes / (prep_ms * 1e-3) / 1e9
+        return {"kernel": "scenario_prepare_kernel", "kernel_ms": round(prep_ms, 4), "algorithmic_gbs": round(gbs, 2),
+                "frac": gbs / HBM_PEAK_GBS}
+
+
+# ----------------------------------------------------------------- check leg
+def oracle_check(wl, orc, lo, hi, exit_h, xt_h, info_h, nthreads):
+    """oracle on solves [lo, hi): (seconds, max dx over successful solves, max dx over failed solves
+    that took the same path on both sides, agreeing exit codes, compared)"""
+    prm, wrm, xin = wl.host_inputs(lo, hi)
+    tc = time.perf_counter()
+    ref = orc.solve_batch(prm, wrm, xin, nthreads=nthreads)
+    sec = time.perf_counter() - tc
+    ex, xt, inf = exit_h[lo:hi], xt_h[lo:hi], info_h[lo:hi]
+    same = ref["status"] == ex
+    dx = np.abs(xt - ref["xtraj"]).reshape(len(ex), -1).max(1)
+    ok = same & (ex == 1)
+    # failed solves that took the same path on both sides with every accepted step from a
+    # converged QP (no max-iter QP): their last iterates must agree like successful ones
+    path = (same & (ex != 1) & (inf[:, 0] == ref["sqp_iter"]) & (inf[:, 1] == ref["qp_iter"]) &
+            (inf[:, 3] == 0) & (ref["qp_maxiter"] == 0))
+    return (sec, float(dx[ok].max()) if ok.any() else 0.0, float(dx[path].max()) if path.any() else 0.0,
+            int(same.sum()), len(ex))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default="C2", choices=sorted(DEFAULT_SCENES))
     ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2: 1024, C3: 4096, C4: 2048, C5: 2048)")
     ap.add_argument("--guesses", type=int, default=8)
+    ap.add_argument("--qp-warm-start", type=int, default=0, choices=(0, 2),
+                    help="IPM start: 0 cold (default), 2 the restated HPIPM warm start (DESIGN.md §2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the oracle (CPU baseline and parity)")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default profiles/traffic_<config>.json)")
     args = ap.parse_args()
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
 
+    # one process per GPU: --gpus must match the launcher's world size (checked before any GPU call)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as `python -m "
+                 f"torch.distributed.run --nnodes=1 --nproc-per-node {args.gpus} --master-addr 127.0.0.1 "
+                 f"bench.py --gpus {args.gpus} ...` (one rank per GPU)")
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -82,476 +373,121 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    from oscar_mpc_planner_mr_modification_amd import native
-    from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners, winner_records, winner_width
     from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
-    from oscar_mpc_planner_mr_modification_amd.producers import prepare_host
-    from oscar_mpc_planner_mr_modification_amd.synthetic import (DECELERATION, ROBOT_RADIUS, SETTINGS_WEIGHTS,
-                                                                 concat_scenes, make_scenes)
 
     lay = config_layout(args.config)
-    if args.config == "C5":
-        return run_shmpc(args, lay, world, rank, dev)
-    if args.config == "C3":
-        return run_c3(args, lay, world, rank, dev)
-    # BASELINE.json configs[3]: 16384 scenes over 8 GPUs -> 2048 per GPU for C4
-    S, G, N = args.scenes or (2048 if args.config == "C4" else 1024), args.guesses, lay.N
-    B = S * G
-    W_CONS, SEL_W = SETTINGS_WEIGHTS["consistency"], 0.75   # guidance_planner.yaml:37 selection weight
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    t0 = time.time()
-    workers = min(threads, 16)
-    if workers > 1 and S >= 2 * workers:
-        from concurrent.futures import ProcessPoolExecutor
-        chunks = np.array_split(np.arange(S), workers)
-        with ProcessPoolExecutor(max_workers=workers) as ex:
-            scenes = concat_scenes(list(ex.map(make_scenes, [lay] * len(chunks), [len(c) for c in chunks],
-                                               [G] * len(chunks), [None] * len(chunks), [20251212] * len(chunks),
-                                               [rank * S + int(c[0]) for c in chunks])))
-    else:
-        scenes = make_scenes(lay, S, G, first_scene=rank * S)
-    gen_s = time.time() - t0
-    dsc = native.scenes_to_device(scenes, dev)
-    pr = native.problem_from_layout(lay)
-    prep = dict(params=torch.empty((B, N, lay.npar), dtype=torch.float64, device=dev),
-                warm=torch.empty((B, N + 1, 7), dtype=torch.float64, device=dev),
-                xinit=torch.empty((B, 5), dtype=torch.float64, device=dev),
-                prev_interp=torch.empty((S, N, 2), dtype=torch.float64, device=dev),
-                consistency_active=torch.empty((B,), dtype=torch.uint8, device=dev))
-    out = dict(xtraj=torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev),
-               utraj=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
-               pobj=torch.empty((B,), dtype=torch.float64, device=dev),
-               exit=torch.empty((B,), dtype=torch.int32, device=dev),
-               info=torch.empty((B, 4), dtype=torch.int32, device=dev))
-    win_w = winner_width(N)
-    winners = torch.empty((S, win_w), dtype=torch.float64, device=dev)
-    gathered = torch.empty((S * world, win_w), dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_p = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-
-    def step(i=None):
-        if i is not None:
-            ev_p[i].record(stream)
-        native.prepare_device(pr, dsc, ROBOT_RADIUS, W_CONS, DECELERATION, out=prep, stream=stream)
-        if i is not None:
-            ev_s[i].record(stream)
-        native.solve_batch_device(pr, prep["params"], prep["warm"], prep["xinit"], out=out, stream=stream)
-        if i is not None:
-            ev_e[i].record(stream)
-        best, _ = native.select_best_device(S, G, N, out["xtraj"], out["pobj"], out["exit"],
-                                            prev_traj=prep["prev_interp"], w_cons=W_CONS,
-                                            consistency_enabled=prep["consistency_active"],
-                                            previously_selected=dsc["previously_selected"], selection_weight=SEL_W,
-                                            stream=stream)
-        winner_records(out["xtraj"], out["utraj"], out["pobj"], best, G, out=winners)
-        if world > 1:
-            gather_winners(winners, world, out=gathered)
+    cls = {"C3": C3Workload, "C5": ShmpcWorkload}.get(args.config, TmpcWorkload)
+    wl = cls(args, lay, rank, world, dev)
+    wl.stream = torch.cuda.current_stream(dev)
+    n_ev = len(wl.phases) + 1
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] for _ in range(args.steps)]
 
     for _ in range(args.warmup):
-        step()
+        wl.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        wl.step(evs[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))
-    prep_ms = float(np.mean([ev_p[i].elapsed_time(ev_s[i]) for i in range(args.steps)]))
+    # per-phase kernel times from HIP events on the launch stream
+    phase_ms = {p: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs])) for j, p in enumerate(wl.phases)}
     if world > 1:
-        te = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        te = torch.tensor([elapsed] + [phase_ms[p] for p in wl.phases], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(te[0]), float(te[1])
-
-    total = args.steps * B * world
-    value = total / elapsed
-    exit_h = out["exit"].cpu().numpy()
-    xt_h = out["xtraj"].cpu().numpy()
-    info_h = out["info"].cpu().numpy()
+        elapsed = float(te[0])
+        phase_ms = {p: float(te[1 + j]) for j, p in enumerate(wl.phases)}
+    kern_ms = phase_ms["solve"]
+    B = wl.B
+    value = args.steps * B * world / elapsed
+    exit_h, xt_h, info_h = (wl.out[k].cpu().numpy() for k in ("exit", "xtraj", "info"))
 
     bps = algorithmic_bytes_per_solve(lay)
     achieved = bps * B / (kern_ms * 1e-3) / 1e9
-    traffic, f64 = None, None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("batch") == B:
-                traffic = tj.get("hbm_bytes_per_launch")
-                f64 = tj.get("fp64_issued_flop_per_launch")
-        except Exception:
-            traffic, f64 = None, None
+    traffic, f64, counters = load_counters(args.traffic_json, args.config, B)
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "sqp_kernel", "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps}
-
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sqp_kernel",
+                "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps, "counters": counters}
     if f64:
-        # the path is fp64-VALU / latency bound: issued fp64 FLOP/s of the
-        # solve kernel (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, profiles/) against the vector peak
-        roofline["fp64_valu"] = {"achieved_tflops": round(f64 / (kern_ms * 1e-3) / 1e12, 3),
-                                 "peak_tflops": FP64_VALU_PEAK_TFLOPS,
-                                 "frac": f64 / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS}
+        # the path is fp64-VALU / latency bound: issued fp64 FLOP/s of the solve kernel
+        # (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) against the vector peak
+        roofline["fp64_valu_issued"] = {"achieved_tflops": round(f64 / (kern_ms * 1e-3) / 1e12, 3),
+                                        "peak_tflops": FP64_VALU_PEAK_TFLOPS,
+                                        "frac": f64 / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS}
+    if "prepare" in phase_ms and hasattr(wl, "producer_roofline"):
+        roofline["producer"] = wl.producer_roofline(phase_ms["prepare"])
+    ok = exit_h == 1
+    stats = {"success_frac": float(ok.mean()), "rti_iters_per_solve": float(info_h[:, 0].mean()),
+             "qp_iters_per_solve": float(info_h[:, 1].mean()), "qp_warm_start": args.qp_warm_start,
+             "scene_gen_s": round(wl.gen_s, 2)}
+    if isinstance(wl, ShmpcWorkload):
+        stats["scene_feasible_frac"] = float((wl.best.cpu().numpy() >= 0).mean())
+    if isinstance(wl, TmpcWorkload):
+        stats["scene_feasible_frac"] = float(ok.reshape(-1, wl.G).any(1).mean())
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
+        "ranks_seen": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (seeded scenes, SURVEY.md §8d)",
-        "config": {"workload": f"{args.config}: jackal unicycle T-MPC++, N={N}, {lay.max_obstacles} obstacles, "
-                               f"{S} scenes x {G} guesses per GPU, 10 SQP-RTI iterations",
-                   "scenes_per_gpu": S, "guesses": G, "N": N, "obstacles": lay.max_obstacles,
-                   "parallelism": f"scene-sharded x{world}" + (" + RCCL all-gather of winners" if world > 1 else "")},
+        "data": f"synthetic (seeded scenes, SURVEY.md §8d {args.config})",
+        "config": dict({"workload": wl.workload}, **wl.config,
+                       parallelism=f"scene-sharded x{world}" + (" + RCCL all-gather of winners" if world > 1 else "")),
         "roofline": roofline,
-        "solver_stats": {"success_frac": float((exit_h == 1).mean()), "qp_iters_per_solve": float(info_h[:, 1].mean()),
-                         "scene_gen_s": round(gen_s, 2)},
-        "phases_ms": {"prepare": round(prep_ms, 4), "solve": round(kern_ms, 4)},
+        "solver_stats": stats,
+        "phases_ms": {p: round(v, 4) for p, v in phase_ms.items()},
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
 
         oracle_py.build()
-        orc = oracle_py.Oracle(lay)
-        hb = prepare_host(lay, scenes, ROBOT_RADIUS, W_CONS, DECELERATION)
+        orc = oracle_py.Oracle(lay, qp_warm_start=args.qp_warm_start)
+        threads = wl.threads
+        if world == 1:
+            # CPU baseline: chunks of the same batch until ~cpu_seconds of CPU work, checked on the way
+            done, t_cpu, dx_ok, dx_fail, agree, compared = 0, 0.0, 0.0, 0.0, 0, 0
+            while done < B and t_cpu < args.cpu_seconds:
+                hi = min(B, done + CHECK_CHUNK)
+                sec, a, f, g, n = oracle_check(wl, orc, done, hi, exit_h, xt_h, info_h, threads)
+                t_cpu += sec
+                dx_ok, dx_fail, agree, compared = max(dx_ok, a), max(dx_fail, f), agree + g, compared + n
+                done = hi
 
-        class _B:  # host copy of the solver inputs the GPU prepared
-            params, warm, xinit = hb.params, hb.warm, hb.xinit
-        b = _B()
-        # bounded sample: chunks of the same batch until ~cpu_seconds of CPU work
-        done, t_cpu, chunk = 0, 0.0, 256
-        max_abs_dx, agree, compared = 0.0, 0, 0
-        while done < B and t_cpu < args.cpu_seconds:
-            sl = slice(done, min(B, done + chunk))
-            tc = time.perf_counter()
-            ref = orc.solve_batch(b.params[sl], b.warm[sl], b.xinit[sl], nthreads=threads)
-            t_cpu += time.perf_counter() - tc
-            ok = (ref["status"] == 1) & (exit_h[sl] == 1)
-            if ok.any():
-                max_abs_dx = max(max_abs_dx, float(np.abs(xt_h[sl][ok] - ref["xtraj"][ok]).max()))
-            agree += int((ref["status"] == exit_h[sl]).sum())
-            compared += len(ref["status"])
-            done = sl.stop
-        # also 1 thread and 8 threads (the reference's num_threads(8))
-        def rate(n, nthreads):
-            tc = time.perf_counter()
-            orc.solve_batch(b.params[:n], b.warm[:n], b.xinit[:n], nthreads=nthreads)
-            return n / (time.perf_counter() - tc)
+            def rate(n, nthreads):
+                prm, wrm, xin = wl.host_inputs(0, min(n, B))
+                tc = time.perf_counter()
+                orc.solve_batch(prm, wrm, xin, nthreads=nthreads)
+                return len(prm) / (time.perf_counter() - tc)
 
-        r1 = rate(64, 1)
-        r8 = rate(512, 8) if threads >= 8 else None
-        result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
-                                  "kind": "port",
-                                  "sample": f"first {done} of the {B} solves of this batch, C oracle "
-                                            f"(same algorithm), OpenMP {threads} threads",
-                                  "single_thread_solves_per_s": round(r1, 2),
-                                  "eight_thread_solves_per_s": None if r8 is None else round(r8, 2)}
-        result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
-                            "solves_compared": compared, "tolerance": 1e-4}
-        result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
-    if rank == 0:
-        print(json.dumps(result))
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def run_c3(args, lay, world, rank, dev):
-    """C3: one batched solve of every scene's bicycle CA-MPC problem + the gather of the results.
-    The decomp halfspaces come from DecompUtil (external) on the host: the per-scene solver
-    inputs are built once on the host and resident in HBM before the timed region."""
-    import torch
-    import torch.distributed as dist
-
-    from oscar_mpc_planner_mr_modification_amd import native
-    from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch
-    from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners, winner_records, winner_width
-
-    S, N, nx, nu = args.scenes or 4096, lay.N, lay.nx, lay.nu
-    B = S
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    t0 = time.time()
-    b = make_c3_batch(lay, S, first_scene=rank * S)
-    gen_s = time.time() - t0
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    d_par, d_warm, d_xi = t(b.params), t(b.warm), t(b.xinit)
-    pr = native.problem_from_layout(lay)
-    out = dict(xtraj=torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev),
-               utraj=torch.empty((B, N, nu), dtype=torch.float64, device=dev),
-               pobj=torch.empty((B,), dtype=torch.float64, device=dev),
-               exit=torch.empty((B,), dtype=torch.int32, device=dev),
-               info=torch.empty((B, 4), dtype=torch.int32, device=dev))
-    win_w = winner_width(N, nx, nu)
-    winners = torch.empty((S, win_w), dtype=torch.float64, device=dev)
-    gathered = torch.empty((S * world, win_w), dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
-
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
-        native.solve_batch_device(pr, d_par, d_warm, d_xi, out=out, stream=stream)
-        if i is not None:
-            ev[i][1].record(stream)
-        best = torch.where(out["exit"] == 1, 0, -1).to(torch.int32)
-        winner_records(out["xtraj"], out["utraj"], out["pobj"], best, 1, out=winners)
-        if world > 1:
-            gather_winners(winners, world, out=gathered)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    if world > 1:
-        te = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(te[0]), float(te[1])
-    value = args.steps * B * world / elapsed
-    exit_h, xt_h, info_h = out["exit"].cpu().numpy(), out["xtraj"].cpu().numpy(), out["info"].cpu().numpy()
-    bps = algorithmic_bytes_per_solve(lay)
-    achieved = bps * B / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("batch") == B:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (seeded scenes, SURVEY.md §8d C3)",
-        "config": {"workload": f"C3: BicycleModel2ndOrderCurvatureAware + CA-MPC contouring + {lay.n_scen} decomp "
-                               f"halfspaces, N={N}, {S} scenes per GPU, 10 SQP-RTI iterations",
-                   "scenes_per_gpu": S, "N": N,
-                   "parallelism": f"scene-sharded x{world}" + (" + RCCL all-gather of results" if world > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sqp_kernel",
-                     "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps},
-        "solver_stats": {"success_frac": float((exit_h == 1).mean()), "qp_iters_per_solve": float(info_h[:, 1].mean()),
-                         "scene_gen_s": round(gen_s, 2)},
-        "phases_ms": {"solve": round(kern_ms, 4)},
-    }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle_py
-
-        oracle_py.build()
-        orc = oracle_py.Oracle(lay)
-        done, t_cpu, chunk = 0, 0.0, 256
-        max_abs_dx, agree, compared = 0.0, 0, 0
-        while done < B and t_cpu < args.cpu_seconds:
-            sl = slice(done, min(B, done + chunk))
-            tc = time.perf_counter()
-            ref = orc.solve_batch(b.params[sl], b.warm[sl], b.xinit[sl], nthreads=threads)
-            t_cpu += time.perf_counter() - tc
-            ok = (ref["status"] == 1) & (exit_h[sl] == 1)
-            if ok.any():
-                max_abs_dx = max(max_abs_dx, float(np.abs(xt_h[sl][ok] - ref["xtraj"][ok]).max()))
-            agree += int((ref["status"] == exit_h[sl]).sum())
-            compared += len(ref["status"])
-            done = sl.stop
-        tc = time.perf_counter()
-        orc.solve_batch(b.params[:64], b.warm[:64], b.xinit[:64], nthreads=1)
-        r1 = 64 / (time.perf_counter() - tc)
-        result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
-                                  "kind": "port",
-                                  "sample": f"first {done} of the {B} solves of this batch, C oracle (same algorithm), "
-                                            f"OpenMP {threads} threads",
-                                  "single_thread_solves_per_s": round(r1, 2)}
-        result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
-                            "solves_compared": compared, "tolerance": 1e-4}
-        result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
-    if rank == 0:
-        print(json.dumps(result))
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def run_shmpc(args, lay, world, rank, dev):
-    """C5: SH-MPC step = scenario producer (samples -> halfspaces) + solve + lowest-cost pick + gather."""
-    import torch
-    import torch.distributed as dist
-
-    from oscar_mpc_planner_mr_modification_amd import native
-    from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners, winner_records, winner_width
-    from oscar_mpc_planner_mr_modification_amd.scenario import (OBSTACLE_RADIUS, PARALLEL_SOLVERS, ROBOT_RADIUS,
-                                                                ScenarioScenes, make_shmpc_scenes,
-                                                                prepare_scenario_host)
-    from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION
-
-    S, P, N, nx = args.scenes or 2048, PARALLEL_SOLVERS, lay.N, lay.nx
-    B = S * P
-    n_obs, n_samples = 12, 100
-    radius = ROBOT_RADIUS + OBSTACLE_RADIUS
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    t0 = time.time()
-    workers = min(threads, 16)
-    first = rank * S
-    if workers > 1 and S >= 2 * workers:
-        from concurrent.futures import ProcessPoolExecutor
-        chunks = [c for c in np.array_split(np.arange(S), workers) if len(c)]
-        with ProcessPoolExecutor(max_workers=workers) as ex:
-            parts = list(ex.map(make_shmpc_scenes, [lay] * len(chunks), [len(c) for c in chunks],
-                                [P] * len(chunks), [n_obs] * len(chunks), [n_samples] * len(chunks),
-                                [20251212] * len(chunks), [first + int(c[0]) for c in chunks]))
-        scenes = ScenarioScenes(stage_params=np.concatenate([q.stage_params for q in parts]),
-                                state=np.concatenate([q.state for q in parts]),
-                                samples=np.concatenate([q.samples for q in parts]), n_solvers=P)
-        del parts
-    else:
-        scenes = make_shmpc_scenes(lay, S, P, n_obs, n_samples, first_scene=first)
-    gen_s = time.time() - t0
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    d_sp, d_st, d_smp = t(scenes.stage_params), t(scenes.state), t(scenes.samples)
-    pr = native.problem_from_layout(lay)
-    prep = dict(params=torch.empty((B, N, lay.npar), dtype=torch.float64, device=dev),
-                warm=torch.empty((B, N + 1, lay.nvar), dtype=torch.float64, device=dev),
-                xinit=torch.empty((B, nx), dtype=torch.float64, device=dev))
-    out = dict(xtraj=torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev),
-               utraj=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
-               pobj=torch.empty((B,), dtype=torch.float64, device=dev),
-               exit=torch.empty((B,), dtype=torch.int32, device=dev),
-               info=torch.empty((B, 4), dtype=torch.int32, device=dev))
-    best = torch.empty((S,), dtype=torch.int32, device=dev)
-    win_w = winner_width(N, nx)
-    winners = torch.empty((S, win_w), dtype=torch.float64, device=dev)
-    gathered = torch.empty((S * world, win_w), dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
-        native.prepare_scenario_device(pr, P, d_sp, d_st, d_smp, radius, DECELERATION, out=prep, stream=stream)
-        if i is not None:
-            ev[i][1].record(stream)
-        native.solve_batch_device(pr, prep["params"], prep["warm"], prep["xinit"], out=out, stream=stream)
-        if i is not None:
-            ev[i][2].record(stream)
-        native.select_lowest_cost_device(S, P, out["pobj"], out["exit"], out=best, stream=stream)
-        winner_records(out["xtraj"], out["utraj"], out["pobj"], best, P, out=winners)
-        if world > 1:
-            gather_winners(winners, world, out=gathered)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    if world > 1:
-        te = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(te[0]), float(te[1])
-    value = args.steps * B * world / elapsed
-    exit_h, xt_h, info_h = out["exit"].cpu().numpy(), out["xtraj"].cpu().numpy(), out["info"].cpu().numpy()
-    best_h = best.cpu().numpy()
-    prep_h = {k: v.cpu().numpy() for k, v in prep.items()} if (rank == 0 and world == 1 and not args.no_cpu) else None
-    bps = algorithmic_bytes_per_solve(lay)
-    achieved = bps * B / (kern_ms * 1e-3) / 1e9
-    # the producer is the HBM-heavy kernel: every sample read once
-    prep_bytes = B * ((N - 1) * n_obs * n_samples * 16 + N * lay.npar * 8 + (N + 1) * lay.nvar * 8)
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("batch") == B:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (seeded scenes, SURVEY.md §8d C5)",
-        "config": {"workload": f"C5: SH-MPC slack model, N={N}, {lay.n_scen} scenario halfspaces per stage from "
-                               f"{n_obs} obstacles x {n_samples} samples, {S} scenes x {P} parallel solvers per GPU, "
-                               f"10 SQP-RTI iterations",
-                   "scenes_per_gpu": S, "parallel_solvers": P, "N": N,
-                   "parallelism": f"scene-sharded x{world}" + (" + RCCL all-gather of winners" if world > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sqp_kernel",
-                     "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps,
-                     "producer": {"kernel": "scenario_prepare_kernel", "kernel_ms": round(prep_ms, 4),
-                                  "algorithmic_gbs": round(prep_bytes / (prep_ms * 1e-3) / 1e9, 2),
-                                  "frac": prep_bytes / (prep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
-        "solver_stats": {"success_frac": float((exit_h == 1).mean()), "scene_feasible_frac": float((best_h >= 0).mean()),
-                         "qp_iters_per_solve": float(info_h[:, 1].mean()), "scene_gen_s": round(gen_s, 2)},
-        "phases_ms": {"prepare": round(prep_ms, 4), "solve": round(kern_ms, 4)},
-    }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle_py
-
-        oracle_py.build()
-        orc = oracle_py.Oracle(lay)
-        done_sc, t_cpu, chunk = 0, 0.0, 64
-        max_abs_dx, agree, compared, prod_dev = 0.0, 0, 0, 0.0
-        host_b = None
-        while done_sc < S and t_cpu < args.cpu_seconds:
-            sl = slice(done_sc, min(S, done_sc + chunk))
-            bs = slice(sl.start * P, sl.stop * P)
-            if done_sc < 4 * chunk:
-                # producer check on the first chunks: host restatement vs the GPU's inputs
-                sub = ScenarioScenes(stage_params=scenes.stage_params[sl], state=scenes.state[sl],
-                                     samples=scenes.samples[bs], n_solvers=P)
-                hb = prepare_scenario_host(lay, sub, radius, DECELERATION)
-                prod_dev = max(prod_dev, float(np.abs(hb.params - prep_h["params"][bs]).max()),
-                               float(np.abs(hb.warm - prep_h["warm"][bs]).max()))
-            # the oracle solves the GPU producer's inputs, so parity isolates the solve
-            prm, wrm, xin = prep_h["params"][bs], prep_h["warm"][bs], prep_h["xinit"][bs]
-            host_b = (prm, wrm, xin) if host_b is None else host_b
-            tc = time.perf_counter()
-            ref = orc.solve_batch(prm, wrm, xin, nthreads=threads)
-            t_cpu += time.perf_counter() - tc
-            ok = (ref["status"] == 1) & (exit_h[bs] == 1)
-            if ok.any():
-                max_abs_dx = max(max_abs_dx, float(np.abs(xt_h[bs][ok] - ref["xtraj"][ok]).max()))
-            agree += int((ref["status"] == exit_h[bs]).sum())
-            compared += len(ref["status"])
-            done_sc = sl.stop
-        done = done_sc * P
-        tc = time.perf_counter()
-        n1 = min(64, len(host_b[0]))
-        orc.solve_batch(host_b[0][:n1], host_b[1][:n1], host_b[2][:n1], nthreads=1)
-        r1 = n1 / (time.perf_counter() - tc)
-        result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
-                                  "kind": "port",
-                                  "sample": f"first {done} of the {B} solves of this batch (the GPU producer's "
-                                            f"inputs), C oracle (same algorithm), OpenMP {threads} threads",
-                                  "single_thread_solves_per_s": round(r1, 2)}
-        result["parity"] = {"max_abs_dx": max_abs_dx, "exit_agreement": agree / max(1, compared),
-                            "solves_compared": compared, "tolerance": 1e-4,
-                            "producer_max_abs_diff": prod_dev}
-        result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
+            result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
+                                      "kind": "port",
+                                      "sample": f"first {done} of the {B} solves of this batch, C oracle (same "
+                                                f"algorithm), OpenMP {threads} threads",
+                                      "single_thread_solves_per_s": round(rate(64, 1), 2),
+                                      "eight_thread_solves_per_s": round(rate(512, 8), 2) if threads >= 8 else None}
+            result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
+            ranks_checked = 1
+        else:
+            # every rank checks a sample of its own shard; reduced over ranks
+            n = min(RANK_SAMPLE, B)
+            _, dx_ok, dx_fail, agree, compared = oracle_check(wl, orc, 0, n, exit_h, xt_h, info_h, threads)
+            t = torch.tensor([dx_ok, dx_fail, agree, compared, 1.0], dtype=torch.float64, device=dev)
+            tm = t.clone()
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            dx_ok, dx_fail, agree, compared, ranks_checked = float(tm[0]), float(tm[1]), int(t[2]), int(t[3]), int(t[4])
+        result["parity"] = {"max_abs_dx": dx_ok, "max_abs_dx_failed_same_path": dx_fail,
+                            "exit_agreement": agree / max(1, compared), "solves_compared": compared,
+                            "ranks_checked": ranks_checked, "tolerance": 1e-4}
+        if isinstance(wl, ShmpcWorkload):
+            result["parity"]["producer_max_abs_diff"] = wl.producer_check()
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -41,6 +41,15 @@ struct AcadosParameters {
 class Solver {
 public:
     // acados_solver_interface.h:96-124
+    // Filled as the reference fills it (acados_solver_interface.cpp:137, 151-153, 164, 193-194):
+    //   qp_status     the acados QP status of the last RTI iteration, unchanged (0 ok, 1 nan,
+    //                 2 max-iter, 3 min-step), as ocp_nlp_get("qp_status") returns it
+    //   nlp_res       max of the NLP residuals (stationarity, dynamics, inequalities,
+    //   kkt_norm_inf  complementarity) at the last linearisation point (acados computes them
+    //                 in the feedback step; the kernel returns them in mpcg_io.stats)
+    //   sqp_iter      RTI iterations executed since initializeOneIteration
+    //   elapsed_time  host wall time of the last kernel call per RTI iteration (time_tot of one
+    //                 Solver_acados_solve), solvetime = their sum, min_time = their minimum
     struct AcadosInfo {
         double min_time = 1e12;
         double kkt_norm_inf = 0.;
@@ -48,9 +57,10 @@ public:
         int sqp_iter = 0;
         double nlp_res = 0.;
         double solvetime = 0.;
-        int qp_status = 0;        // HPIPM convention: 0 ok, 1 max-iter, 2 min-step, 3 nan
+        int qp_status = 0;
         double pobj{0.};
         int qp_iter = 0;          // total interior-point iterations of the last solve (extra)
+        double res_stat = 0., res_eq = 0., res_ineq = 0., res_comp = 0.;  // the four residuals (extra)
         void print() const;
     };
 
@@ -128,6 +138,8 @@ public:
     const mpcg_problem& problem() const { return _problem; }
     // NLP multipliers carried between solves, [N][nx + nh] (include/mpcg.h, mpcg_io)
     std::vector<double>& multipliers() { return _lam; }
+    // the capsule's QP memory (HPIPM warm start of the next QP), empty after a reset
+    const std::vector<double>& qpMemory() const { return _qp; }
 
 private:
     friend class SolverBatch;
@@ -135,12 +147,13 @@ private:
     mpcg_context* _ctx = nullptr;   // created on the first solve (no GPU needed before)
     std::vector<double> _iterate;   // NLP iterate [u x] per stage, what loadWarmstart loads (ocp_nlp_out x/u)
     std::vector<double> _lam;       // ocp_nlp_out multipliers
+    std::vector<double> _qp;        // QP memory (mpcg_io.qp_out of the last call); empty = fresh / reset
     int _exit_code_one_iter = -1;
     int _raw_status = 0;            // kernel exit code of the last call (already mapped to the 1/0/2/3/4 convention)
 
     int run(int iterations);
     void absorb(const double* xtraj, const double* utraj, double pobj, int exit_code, const int* info,
-                const double* lam);
+                const double* lam, const double* qp, const double* stats, double seconds);
     int model_index(const std::string& name) const;
     bool is_state(const std::string& name) const;
 };
@@ -162,7 +175,7 @@ private:
     mpcg_problem _problem;
     int _max_batch;
     mpcg_context* _ctx = nullptr;
-    std::vector<double> _params, _warm, _xinit, _lam_in, _xtraj, _utraj, _pobj, _lam_out;
+    std::vector<double> _params, _warm, _xinit, _lam_in, _xtraj, _utraj, _pobj, _lam_out, _qp_in, _qp_out, _stats;
     std::vector<int> _exit, _info;
 };
 

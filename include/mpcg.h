@@ -37,7 +37,7 @@ extern "C" {
 #define MPCG_NU 2            /* the unicycle models */
 #define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 4
+#define MPCG_ABI_VERSION 5
 /* mpcg_problem.model */
 #define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
 #define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
@@ -76,11 +76,22 @@ typedef struct mpcg_problem {
     int i_w_tangle, i_w_tcont;     /* terminal_angle / terminal_contouring: read by the bicycle model's
                                       CurvatureAwareContouring at stage N-1 (curvature_aware_contouring.py:94-103,
                                       Forces' per-stage objective, generate_forces_solver.py:50-59) */
+    int qp_warm_start;             /* qp_solver_warm_start (generate_acados_solver.py:173): 2 = HPIPM primal +
+                                      dual warm start of every QP from the previous QP's solution (the capsule's
+                                      QP memory), slacks and multipliers clipped below at qp_ws_thr; the first
+                                      QP of a call starts warm only from mpcg_io.qp_in.  0 = cold start */
+    double qp_ws_thr;              /* 0.1 */
 } mpcg_problem;
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,
- * last QP status (0 ok, 1 nan/diverged, 2 max-iter, 3 min-step), reserved */
+ * last QP status (acados: 0 ok, 1 nan/diverged, 2 max-iter, 3 min-step), and the
+ * number of QPs that stopped at max-iter (their unconverged steps were applied) */
 #define MPCG_INFO_STRIDE 4
+/* per-solve NLP residuals, double x 4, at the last linearisation point with the
+ * multipliers the NLP holds there (acados ocp_nlp_res_compute; their max is what
+ * acados_solver_interface.cpp:151,164 reads as nlp_res / kkt_norm_inf):
+ * stationarity, dynamics (res_eq), inequality violation, complementarity */
+#define MPCG_STATS_STRIDE 4
 
 int mpcg_abi_version(void);
 const char *mpcg_last_error(void);
@@ -90,6 +101,12 @@ int mpcg_num_h(const mpcg_problem *pr);
 
 /* Size in doubles of one solve's multiplier block: N * (nx + nh). */
 int mpcg_lam_size(const mpcg_problem *pr);
+
+/* Size in doubles of one solve's QP memory (mpcg_io.qp_in / qp_out): the last QP's
+ * step, dynamics multipliers and every inequality row's slack and multiplier, in the
+ * kernel's own order (opaque: hand back what a previous solve of the same problem
+ * wrote).  -1 without a compiled instance. */
+int mpcg_qp_mem_size(const mpcg_problem *pr);
 
 /* Fill `pr` from a parameter map (the name -> index pairs of
  * parameter_map.yaml) and the solver settings: the module bundles are found
@@ -130,6 +147,15 @@ typedef struct mpcg_io {
     double *xtraj, *utraj, *pobj;
     int *exit_code, *info;
     double *lam_out;
+    /* ABI 5: the capsule's QP memory [batch][mpcg_qp_mem_size] in / out (HPIPM's qp_sol,
+     * kept between Solver::solve() calls; NULL qp_in = a fresh or reset capsule, whose
+     * first QP starts cold: ocp_nlp_solver_reset_qp_memory, acados_solver_interface.cpp:189),
+     * and the NLP residuals [batch][MPCG_STATS_STRIDE]; each may be NULL.  A solve whose
+     * qp_in block starts with a NaN has no QP memory (mixed batches of fresh and carried
+     * solvers) */
+    const double *qp_in;
+    double *qp_out;
+    double *stats;
 } mpcg_io;
 
 /* Batched solve on device buffers, enqueued on `stream` (hipStream_t, NULL =

@@ -742,19 +742,34 @@ static double max_step(qp_ws *w) {
     return amax;
 }
 
-static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters) {
+static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
     int N = w->N;
-    /* cold start */
-    for (int k = 0; k <= N; k++) {
-        qp_stage *S = &w->st[k];
-        for (int i = 0; i < NZ; i++)
-            if (!(k == 0 && i >= NU)) S->dz[i] = 0.0; /* x0 part stays fixed */
-        for (int i = 0; i < NX; i++) S->pi[i] = 0.0;
-        for (int c = 0; c < S->ni; c++) {
-            double s = S->d[c];
-            for (int i = 0; i < NZ; i++) s -= S->D[c][i] * S->dz[i];
-            S->t[c] = s > pr->qp_thr0 ? s : pr->qp_thr0;
-            S->lam[c] = pr->qp_mu0 / S->t[c];
+    if (!warm) {
+        /* cold start */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int i = 0; i < NZ; i++)
+                if (!(k == 0 && i >= NU)) S->dz[i] = 0.0; /* x0 part stays fixed */
+            for (int i = 0; i < NX; i++) S->pi[i] = 0.0;
+            for (int c = 0; c < S->ni; c++) {
+                double s = S->d[c];
+                for (int i = 0; i < NZ; i++) s -= S->D[c][i] * S->dz[i];
+                S->t[c] = s > pr->qp_thr0 ? s : pr->qp_thr0;
+                S->lam[c] = pr->qp_mu0 / S->t[c];
+            }
+        }
+    } else {
+        /* HPIPM warm_start 2 (d_ocp_qp_ipm init_var): the previous QP solution is the
+         * initial point -- primal step, dynamics multipliers, inequality slacks and
+         * multipliers -- with the slacks and multipliers clipped below at thr0; the
+         * x0 part of the step is the fixed xinit - z_0 */
+        const double thr = pr->qp_ws_thr;
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int c = 0; c < S->ni; c++) {
+                if (S->t[c] < thr) S->t[c] = thr;
+                if (S->lam[c] < thr) S->lam[c] = thr;
+            }
         }
     }
     int status = AC_MAXITER;
@@ -766,6 +781,15 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters) {
         /* non-finite or diverged (infeasible QP: duals blow up) -> NaN status */
         if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { status = AC_NAN; break; }
         if (getenv("ORC_DEBUG")) fprintf(stderr, "  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", it, rs, re, ri, mu);
+        if (getenv("ORC_DEBUG2")) {
+            /* top complementarity contributors */
+            for (int k = 0; k <= N; k++) {
+                qp_stage *S = &w->st[k];
+                for (int c = 0; c < S->ni; c++)
+                    if (S->lam[c] * S->t[c] > 1e-2 * mu * 50)
+                        fprintf(stderr, "     k %d row %d (h %d) t %.3e lam %.3e d %.3e\n", k, c, S->hrow[c], S->t[c], S->lam[c], S->d[c]);
+            }
+        }
         if (rs < pr->qp_tol && re < pr->qp_tol && ri < pr->qp_tol && mu < pr->qp_tol) { status = AC_SUCCESS; break; }
         if (it >= pr->qp_iter_max) { status = AC_MAXITER; break; }
         /* barrier-augmented Hessian */
@@ -842,11 +866,134 @@ int orc_solve(const orc_problem *pr, const double *params, const double *warm, c
 /* side of the single finite bound of h row r: 1 upper, 0 lower */
 static int h_side(const double *uh, int r) { return uh[r] < BIGBOUND ? 1 : 0; }
 
+/* NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
+ * multipliers the NLP holds: dynamics pi, row multipliers lr[k][c] */
+static void nlp_residuals(qp_ws *w, double *const *lr, double *rstat, double *rineq, double *rcomp) {
+    int N = w->N;
+    double s_max = 0.0, i_max = 0.0, c_max = 0.0;
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w->st[k];
+        double r[NZ];
+        for (int i = 0; i < NZ; i++) r[i] = S->g[i];
+        if (k < N)
+            for (int i = 0; i < NZ; i++) {
+                double acc = 0.0;
+                for (int m = 0; m < NX; m++) acc += (i < NU ? S->B[m][i] : S->A[m][i - NU]) * S->pi[m];
+                r[i] += acc;
+            }
+        if (k > 0)
+            for (int i = 0; i < NX; i++) r[NU + i] -= w->st[k - 1].pi[i];
+        for (int c = 0; c < S->ni; c++) {
+            for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * lr[k][c];
+            if (-S->d[c] > i_max) i_max = -S->d[c];
+            if (fabs(lr[k][c] * S->d[c]) > c_max) c_max = fabs(lr[k][c] * S->d[c]);
+        }
+        int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
+        for (int i = i0; i < i1; i++)
+            if (fabs(r[i]) > s_max) s_max = fabs(r[i]);
+    }
+    *rstat = s_max; *rineq = i_max; *rcomp = c_max;
+}
+
+/* SQP preparation phase: the QP of the iterate z (cost gradient / exact Hessian with
+ * MIRROR, shooting defects and sensitivities, bounds and linearised h rows with the
+ * multiplier-weighted Hessians); returns the dynamics residual res_eq */
+static double linearise(const orc_problem *pr, const double *params, double (*z)[NZ], double (*pi)[NX],
+                        const double *lamh, const double *lh, const double *uh, qp_ws *ws, double *hh) {
+    qp_ws w = *ws;
+    int N = pr->N, npar = pr->npar, nh = orc_num_h(pr);
+    double res_eq;
+    double h[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], jac[(ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN) * NZ];
+        res_eq = 0.0;
+    for (int k = 0; k < N; k++) {
+        qp_stage *S = &w.st[k];
+        const double *p = params + (size_t)k * npar;
+        double L, g[NZ], Hc[NZ * NZ], Hd[NZ * NZ], xn[NX], A[NX * NX], B[NX * NU];
+        orc_stage_cost_k(pr, k, z[k], p, &L, g, Hc);
+        orc_discrete(pr, z[k], p, xn, A, B, pi[k], Hd);
+        for (int i = 0; i < NZ; i++) {
+            S->g[i] = g[i];
+            for (int j = 0; j < NZ; j++) S->H[i][j] = Hc[i * NZ + j] + Hd[i * NZ + j];
+        }
+        for (int i = 0; i < NX; i++) {
+            S->b[i] = xn[i] - z[k + 1][NU + i];
+            if (fabs(S->b[i]) > res_eq) res_eq = fabs(S->b[i]);
+            for (int j = 0; j < NX; j++) S->A[i][j] = A[i * NX + j];
+            for (int j = 0; j < NU; j++) S->B[i][j] = B[i * NU + j];
+        }
+        int ni = 0;
+        /* input bounds (idxbu = all, :104-107) */
+        for (int i = 0; i < NU; i++) {
+            memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = -1.0;
+            S->d[ni] = z[k][i] - pr->lbu[i]; S->hrow[ni] = -1; ni++;
+            memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = 1.0;
+            S->d[ni] = pr->ubu[i] - z[k][i]; S->hrow[ni] = -1; ni++;
+        }
+        if (k >= 1) {
+            /* state bounds on stages 1..N-1 (idxbx = all, :100-102) */
+            for (int i = 0; i < NX; i++) {
+                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = -1.0;
+                S->d[ni] = z[k][NU + i] - pr->lbx[i]; S->hrow[ni] = -1; ni++;
+                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = 1.0;
+                S->d[ni] = pr->ubx[i] - z[k][NU + i]; S->hrow[ni] = -1; ni++;
+            }
+            /* nonlinear constraints h, linearised; Hessian weighted by the
+             * NLP multipliers (exact Hessian of the Lagrangian) */
+            orc_stage_constraints(pr, z[k], p, h, jac, hh);
+            for (int r = 0; r < nh; r++) {
+                double wgt = lamh[(size_t)k * 2 * nh + 2 * r + 1] - lamh[(size_t)k * 2 * nh + 2 * r + 0];
+                if (wgt != 0.0)
+                    for (int i = 0; i < NZ; i++)
+                        for (int j = 0; j < NZ; j++) S->H[i][j] += wgt * hh[(size_t)r * NZ * NZ + i * NZ + j];
+                if (uh[r] < BIGBOUND) {
+                    for (int i = 0; i < NZ; i++) S->D[ni][i] = jac[r * NZ + i];
+                    S->d[ni] = uh[r] - h[r]; S->hrow[ni] = r; S->hsgn[ni] = 1; ni++;
+                }
+                if (lh[r] > -BIGBOUND) {
+                    for (int i = 0; i < NZ; i++) S->D[ni][i] = -jac[r * NZ + i];
+                    S->d[ni] = h[r] - lh[r]; S->hrow[ni] = r; S->hsgn[ni] = 0; ni++;
+                }
+            }
+        }
+        S->ni = ni;
+        double Hf[NZ * NZ];
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NZ; j++) Hf[i * NZ + j] = S->H[i][j];
+        orc_mirror(NZ, Hf, pr->reg_eps);
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NZ; j++) S->H[i][j] = Hf[i * NZ + j];
+    }
+    /* terminal stage: no cost (cost_type_e default), no constraints,
+     * zero Hessian mirrored to eps*I */
+    {
+        qp_stage *S = &w.st[N];
+        memset(S->H, 0, sizeof S->H);
+        memset(S->g, 0, sizeof S->g);
+        double Hx[NX * NX] = {0};
+        orc_mirror(NX, Hx, pr->reg_eps);
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++) S->H[NU + i][NU + j] = Hx[i * NX + j];
+        S->ni = 0;
+    }
+    return res_eq;
+}
+
+int orc_qp_mem_size(const orc_problem *pr) {
+    return (pr->N + 1) * (NZ + NX + 2 * (2 * NZ + 2 * orc_num_h(pr)));
+}
+
 int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
                  const double *lam_in, double *xtraj, double *utraj, double *lam_out, orc_info *info) {
+    return orc_solve_full(pr, params, warm, xinit, lam_in, NULL, xtraj, utraj, lam_out, NULL, info);
+}
+
+int orc_solve_full(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
+                   const double *lam_in, const double *qp_in, double *xtraj, double *utraj, double *lam_out,
+                   double *qp_out, orc_info *info) {
     int N = pr->N, npar = pr->npar;
     int nh = orc_num_h(pr);
     int maxi = 2 * NZ + 2 * nh;
+    const int qstride = NZ + NX + 2 * maxi;  /* orc_qp_mem_size per stage */
     double lh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], uh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN];
     orc_h_bounds(pr, lh, uh);
 
@@ -885,92 +1032,51 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
         }
     }
 
-    double h[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], jac[(ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN) * NZ];
+    /* the capsule's QP memory (HPIPM's qp_sol: step, pi, slacks, multipliers of the last QP) */
+    int have_qp = 0;
+    if (qp_in && pr->qp_warm_start == 2 && !isnan(qp_in[0])) {
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w.st[k];
+            const double *q = qp_in + (size_t)k * qstride;
+            memcpy(S->dz, q, sizeof(double) * NZ);
+            memcpy(S->pi, q + NZ, sizeof(double) * NX);
+            memcpy(S->t, q + NZ + NX, sizeof(double) * maxi);
+            memcpy(S->lam, q + NZ + NX + maxi, sizeof(double) * maxi);
+        }
+        have_qp = 1;
+    }
+    double *lrow = (double *)calloc((size_t)(N + 1) * maxi, sizeof(double));
+    double *lrp[ORC_MAX_N + 1];
+    for (int k = 0; k <= N; k++) lrp[k] = lrow + (size_t)k * maxi;
+    double res_stat = 0.0, res_ineq = 0.0, res_comp = 0.0;
+
     double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
-    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0;
+    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0, n_maxit = 0;
     double res_eq = 0.0;
 
     for (int it = 0; it < pr->sqp_iters; it++) {
-        /* ---- linearise at z (preparation phase) ---- */
-        res_eq = 0.0;
-        for (int k = 0; k < N; k++) {
-            qp_stage *S = &w.st[k];
-            const double *p = params + (size_t)k * npar;
-            double L, g[NZ], Hc[NZ * NZ], Hd[NZ * NZ], xn[NX], A[NX * NX], B[NX * NU];
-            orc_stage_cost_k(pr, k, z[k], p, &L, g, Hc);
-            orc_discrete(pr, z[k], p, xn, A, B, pi[k], Hd);
-            for (int i = 0; i < NZ; i++) {
-                S->g[i] = g[i];
-                for (int j = 0; j < NZ; j++) S->H[i][j] = Hc[i * NZ + j] + Hd[i * NZ + j];
-            }
-            for (int i = 0; i < NX; i++) {
-                S->b[i] = xn[i] - z[k + 1][NU + i];
-                if (fabs(S->b[i]) > res_eq) res_eq = fabs(S->b[i]);
-                for (int j = 0; j < NX; j++) S->A[i][j] = A[i * NX + j];
-                for (int j = 0; j < NU; j++) S->B[i][j] = B[i * NU + j];
-            }
-            int ni = 0;
-            /* input bounds (idxbu = all, :104-107) */
-            for (int i = 0; i < NU; i++) {
-                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = -1.0;
-                S->d[ni] = z[k][i] - pr->lbu[i]; S->hrow[ni] = -1; ni++;
-                memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][i] = 1.0;
-                S->d[ni] = pr->ubu[i] - z[k][i]; S->hrow[ni] = -1; ni++;
-            }
-            if (k >= 1) {
-                /* state bounds on stages 1..N-1 (idxbx = all, :100-102) */
-                for (int i = 0; i < NX; i++) {
-                    memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = -1.0;
-                    S->d[ni] = z[k][NU + i] - pr->lbx[i]; S->hrow[ni] = -1; ni++;
-                    memset(S->D[ni], 0, sizeof(double) * NZ); S->D[ni][NU + i] = 1.0;
-                    S->d[ni] = pr->ubx[i] - z[k][NU + i]; S->hrow[ni] = -1; ni++;
-                }
-                /* nonlinear constraints h, linearised; Hessian weighted by the
-                 * NLP multipliers (exact Hessian of the Lagrangian) */
-                orc_stage_constraints(pr, z[k], p, h, jac, hh);
-                for (int r = 0; r < nh; r++) {
-                    double wgt = lamh[(size_t)k * 2 * nh + 2 * r + 1] - lamh[(size_t)k * 2 * nh + 2 * r + 0];
-                    if (wgt != 0.0)
-                        for (int i = 0; i < NZ; i++)
-                            for (int j = 0; j < NZ; j++) S->H[i][j] += wgt * hh[(size_t)r * NZ * NZ + i * NZ + j];
-                    if (uh[r] < BIGBOUND) {
-                        for (int i = 0; i < NZ; i++) S->D[ni][i] = jac[r * NZ + i];
-                        S->d[ni] = uh[r] - h[r]; S->hrow[ni] = r; S->hsgn[ni] = 1; ni++;
-                    }
-                    if (lh[r] > -BIGBOUND) {
-                        for (int i = 0; i < NZ; i++) S->D[ni][i] = -jac[r * NZ + i];
-                        S->d[ni] = h[r] - lh[r]; S->hrow[ni] = r; S->hsgn[ni] = 0; ni++;
-                    }
-                }
-            }
-            S->ni = ni;
-            double Hf[NZ * NZ];
-            for (int i = 0; i < NZ; i++)
-                for (int j = 0; j < NZ; j++) Hf[i * NZ + j] = S->H[i][j];
-            orc_mirror(NZ, Hf, pr->reg_eps);
-            for (int i = 0; i < NZ; i++)
-                for (int j = 0; j < NZ; j++) S->H[i][j] = Hf[i * NZ + j];
-        }
-        /* terminal stage: no cost (cost_type_e default), no constraints,
-         * zero Hessian mirrored to eps*I */
-        {
-            qp_stage *S = &w.st[N];
-            memset(S->H, 0, sizeof S->H);
-            memset(S->g, 0, sizeof S->g);
-            double Hx[NX * NX] = {0};
-            orc_mirror(NX, Hx, pr->reg_eps);
-            for (int i = 0; i < NX; i++)
-                for (int j = 0; j < NX; j++) S->H[NU + i][NU + j] = Hx[i * NX + j];
-            S->ni = 0;
-        }
+        res_eq = linearise(pr, params, z, pi, lamh, lh, uh, &w, hh);
         /* x0 elimination: lbx_0 = ubx_0 = xinit (acados_solver_interface.cpp:124-125) */
         for (int i = 0; i < NX; i++) w.st[0].dz[NU + i] = xinit[i] - z[0][NU + i];
 
+        /* NLP residuals with the NLP's multipliers: the dynamics pi; per row the previous
+         * QP's multiplier (FIXED_STEP: lam = lam_qp), else the carried h-row ones (box 0) */
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w.st[k];
+            if (k < N && !have_qp) memcpy(S->pi, pi[k], sizeof(double) * NX);
+            for (int c = 0; c < S->ni; c++)
+                lrp[k][c] = have_qp ? S->lam[c]
+                                    : (S->hrow[c] >= 0 ? lamh[(size_t)k * 2 * nh + 2 * S->hrow[c] + S->hsgn[c]] : 0.0);
+        }
+        nlp_residuals(&w, lrp, &res_stat, &res_ineq, &res_comp);
+
         /* ---- feedback phase: QP ---- */
         int qit = 0;
-        qp_status = qp_solve(pr, &w, &qit);
+        qp_status = qp_solve(pr, &w, &qit, have_qp && pr->qp_warm_start == 2);
+        have_qp = 1;
         qp_iter_total += qit;
         sqp_iter++;
+        n_maxit += qp_status == AC_MAXITER;
         if (qp_status != AC_SUCCESS && qp_status != AC_MAXITER) {
             acados_status = AC_QP_FAILURE;
             break;
@@ -1009,6 +1115,18 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
         }
     }
 
+    if (qp_out) {
+        for (int k = 0; k <= N; k++) {
+            qp_stage *S = &w.st[k];
+            double *q = qp_out + (size_t)k * qstride;
+            memcpy(q, S->dz, sizeof(double) * NZ);
+            memcpy(q + NZ, S->pi, sizeof(double) * NX);
+            memcpy(q + NZ + NX, S->t, sizeof(double) * maxi);
+            memcpy(q + NZ + NX + maxi, S->lam, sizeof(double) * maxi);
+        }
+    }
+    free(lrow);
+
     int exit_code = acados_status;
     if (res_eq > pr->res_eq_fail && exit_code == AC_SUCCESS) exit_code = AC_QP_FAILURE;
     if (exit_code == AC_SUCCESS) exit_code = 1;
@@ -1019,6 +1137,10 @@ int orc_solve_ex(const orc_problem *pr, const double *params, const double *warm
         info->qp_status = qp_status;
         info->res_eq = res_eq;
         info->pobj = pobj;
+        info->res_stat = res_stat;
+        info->res_ineq = res_ineq;
+        info->res_comp = res_comp;
+        info->qp_maxiter = n_maxit;
     }
     free(hh); free(lamh); free(pi); free(z);
     free(ibl); free(dbl); free(Dall); free(w.st);
@@ -1063,4 +1185,88 @@ void orc_solve_batch_ex(const orc_problem *pr, int batch, const double *params, 
         if (qp_iters) qp_iters[b] = info.qp_iter_total;
     }
     (void)nthreads;
+}
+
+void orc_solve_batch_full(const orc_problem *pr, int batch, const double *params, const double *warm,
+                          const double *xinit, const double *lam_in, const double *qp_in, double *xtraj,
+                          double *utraj, int *status, double *lam_out, double *qp_out, orc_info *infos,
+                          int nthreads) {
+    int N = pr->N;
+    size_t LS = (size_t)N * (NX + orc_num_h(pr)), QS = (size_t)orc_qp_mem_size(pr);
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+#endif
+    for (int b = 0; b < batch; b++) {
+        orc_info info;
+        status[b] = orc_solve_full(pr, params + (size_t)b * N * pr->npar, warm + (size_t)b * (N + 1) * NZ,
+                                   xinit + (size_t)b * NX, lam_in ? lam_in + b * LS : NULL,
+                                   qp_in ? qp_in + b * QS : NULL, xtraj + (size_t)b * (N + 1) * NX,
+                                   utraj + (size_t)b * N * NU, lam_out ? lam_out + b * LS : NULL,
+                                   qp_out ? qp_out + b * QS : NULL, &info);
+        if (infos) infos[b] = info;
+    }
+    (void)nthreads;
+}
+
+/* Diagnostics: the first QP of a solve (the linearisation at the warm start), for an
+ * independent feasibility check (scripts/qp_feasibility.py, HiGHS LP).  A [N][NX][NX],
+ * B [N][NX][NU], b [N][NX], D [(N+1)][maxi][NZ], d [(N+1)][maxi], ni [N+1], dx0 [NX];
+ * rows are D_c dz <= d_c.  Returns maxi = 2 NZ + 2 nh. */
+int orc_qp_data(const orc_problem *pr, const double *params, const double *warm, const double *xinit,
+                const double *lam_in, double *A, double *B, double *b, double *D, double *d, int *ni,
+                double *dx0) {
+    int N = pr->N, nh = orc_num_h(pr), maxi = 2 * NZ + 2 * nh;
+    double lh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN], uh[ORC_MAX_LIN + ORC_MAX_ELL + ORC_MAX_SCEN];
+    orc_h_bounds(pr, lh, uh);
+    qp_ws w;
+    w.N = N;
+    w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
+    size_t nrow = (size_t)(N + 1) * maxi;
+    double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));
+    double *dbl = (double *)calloc(nrow * 9, sizeof(double));
+    int *ibl = (int *)calloc(nrow * 2, sizeof(int));
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w.st[k];
+        size_t o = (size_t)k * maxi;
+        S->D = Dall + o;
+        S->d = dbl + o; S->t = dbl + nrow + o; S->lam = dbl + 2 * nrow + o;
+        S->dt = dbl + 3 * nrow + o; S->dl = dbl + 4 * nrow + o; S->dt_aff = dbl + 5 * nrow + o;
+        S->dl_aff = dbl + 6 * nrow + o; S->rin = dbl + 7 * nrow + o; S->rc = dbl + 8 * nrow + o;
+        S->hrow = ibl + o; S->hsgn = ibl + nrow + o;
+    }
+    double (*z)[NZ] = (double (*)[NZ])calloc(N + 1, sizeof(double[NZ]));
+    double (*pi)[NX] = (double (*)[NX])calloc(N + 1, sizeof(double[NX]));
+    double *lamh = (double *)calloc((size_t)(N + 1) * 2 * nh, sizeof(double));
+    double *hh = (double *)malloc(sizeof(double) * (nh ? nh : 1) * NZ * NZ);
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < NZ; i++) z[k][i] = warm[k * NZ + i];
+    for (int i = 0; i < NU; i++) z[N][i] = 0.0;
+    const int LS = NX + nh;
+    if (lam_in)
+        for (int k = 0; k < N; k++) {
+            for (int i = 0; i < NX; i++) pi[k][i] = lam_in[(size_t)k * LS + i];
+            if (k >= 1)
+                for (int r = 0; r < nh; r++)
+                    lamh[(size_t)k * 2 * nh + 2 * r + h_side(uh, r)] = lam_in[(size_t)k * LS + NX + r];
+        }
+    linearise(pr, params, z, pi, lamh, lh, uh, &w, hh);
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w.st[k];
+        if (k < N)
+            for (int i = 0; i < NX; i++) {
+                b[k * NX + i] = S->b[i];
+                for (int j = 0; j < NX; j++) A[(k * NX + i) * NX + j] = S->A[i][j];
+                for (int j = 0; j < NU; j++) B[(k * NX + i) * NU + j] = S->B[i][j];
+            }
+        ni[k] = S->ni;
+        for (int c = 0; c < S->ni; c++) {
+            d[(size_t)k * maxi + c] = S->d[c];
+            for (int i = 0; i < NZ; i++) D[((size_t)k * maxi + c) * NZ + i] = S->D[c][i];
+        }
+    }
+    for (int i = 0; i < NX; i++) dx0[i] = xinit[i] - z[0][NU + i];
+    free(hh); free(lamh); free(pi); free(z);
+    free(ibl); free(dbl); free(Dall); free(w.st);
+    return maxi;
 }

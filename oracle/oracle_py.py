@@ -42,12 +42,15 @@ class OrcProblem(C.Structure):
         ("reg_eps", C.c_double), ("qp_mu0", C.c_double), ("qp_thr0", C.c_double),
         ("res_eq_fail", C.c_double),
         ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int), ("nu", C.c_int),
+        ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
     ]
 
 
 class OrcInfo(C.Structure):
     _fields_ = [("sqp_iter", C.c_int), ("qp_iter_total", C.c_int), ("qp_status", C.c_int),
-                ("res_eq", C.c_double), ("pobj", C.c_double)]
+                ("res_eq", C.c_double), ("pobj", C.c_double),
+                ("res_stat", C.c_double), ("res_ineq", C.c_double), ("res_comp", C.c_double),
+                ("qp_maxiter", C.c_int)]
 
 
 def build(force: bool = False) -> str:
@@ -88,6 +91,9 @@ def lib(model: str = "unicycle"):
         L.orc_solve_batch.argtypes = [P, C.c_int, dp, dp, dp, dp, dp, dp, ip, ip, C.c_int]
         vp = C.c_void_p
         L.orc_solve_batch_ex.argtypes = [P, C.c_int, dp, dp, dp, vp, dp, dp, dp, ip, ip, vp, C.c_int]
+        L.orc_solve_batch_full.argtypes = [P, C.c_int, dp, dp, dp, vp, vp, dp, dp, ip, vp, vp, vp, C.c_int]
+        L.orc_qp_mem_size.argtypes = [P]
+        L.orc_qp_mem_size.restype = C.c_int
         L.orc_nx.restype = C.c_int
         L.orc_nu.restype = C.c_int
         if (L.orc_nx(), L.orc_nu()) != MODEL_DIMS[model]:
@@ -122,6 +128,10 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.qp_mu0 = opts.get("qp_mu0", 1.0)
     pr.qp_thr0 = opts.get("qp_thr0", 1.0)
     pr.res_eq_fail = opts.get("res_eq_fail", 1e-2)
+    # IPM start: cold by default; 2 = the restated HPIPM warm start (qp_solver_warm_start,
+    # generate_acados_solver.py:173) with HPIPM's floor (DESIGN.md §2 "QP start")
+    pr.qp_warm_start = opts.get("qp_warm_start", 0)
+    pr.qp_ws_thr = opts.get("qp_ws_thr", 0.1)
     return pr
 
 
@@ -230,29 +240,39 @@ class Oracle:
     def lam_size(self):
         return self.layout.N * (self.nx + self.layout.nh)
 
-    def solve_batch(self, params, warm, xinit, nthreads=0, lam_in=None, return_lam=False):
-        """lam_in / returned lam: [B, N, nx + nh] NLP multipliers (include/mpcg.h, mpcg_io)."""
+    def qp_mem_size(self):
+        return self.L.orc_qp_mem_size(C.byref(self.pr))
+
+    def solve_batch(self, params, warm, xinit, nthreads=0, lam_in=None, return_lam=False, qp_in=None,
+                    return_qp=False):
+        """lam_in / returned lam: [B, N, nx + nh] NLP multipliers (include/mpcg.h, mpcg_io);
+        qp_in / returned qp: [B, qp_mem_size] the capsule's QP memory (oracle layout).
+        Returns trajectories, pobj, status and the per-solve info arrays (sqp_iter,
+        qp_iter, qp_status, res_eq, res_stat, res_ineq, res_comp)."""
         N, nx = self.layout.N, self.nx
         B = params.shape[0]
-        if lam_in is not None or return_lam:
-            xt, ut = np.zeros((B, N + 1, nx)), np.zeros((B, N, self.nu))
-            pobj, st, qi = np.zeros(B), np.zeros(B, np.int32), np.zeros(B, np.int32)
-            li = None if lam_in is None else np.ascontiguousarray(lam_in, float).reshape(B, -1)
-            lo = np.zeros((B, N, nx + self.layout.nh))
-            self.L.orc_solve_batch_ex(C.byref(self.pr), B, np.ascontiguousarray(params, float).reshape(-1),
-                                      np.ascontiguousarray(warm, float).reshape(-1),
-                                      np.ascontiguousarray(xinit, float).reshape(-1),
-                                      None if li is None else li.ctypes.data_as(C.c_void_p),
-                                      xt.reshape(-1), ut.reshape(-1), pobj, st, qi,
-                                      lo.ctypes.data_as(C.c_void_p), nthreads)
-            return dict(xtraj=xt, utraj=ut, pobj=pobj, status=st, qp_iter=qi, lam=lo)
-        xt = np.zeros((B, N + 1, nx))
-        ut = np.zeros((B, N, self.nu))
-        pobj = np.zeros(B)
+        xt, ut = np.zeros((B, N + 1, nx)), np.zeros((B, N, self.nu))
         st = np.zeros(B, np.int32)
-        qi = np.zeros(B, np.int32)
-        self.L.orc_solve_batch(C.byref(self.pr), B, np.ascontiguousarray(params, float).reshape(-1),
-                               np.ascontiguousarray(warm, float).reshape(-1),
-                               np.ascontiguousarray(xinit, float).reshape(-1),
-                               xt.reshape(-1), ut.reshape(-1), pobj, st, qi, nthreads)
-        return dict(xtraj=xt, utraj=ut, pobj=pobj, status=st, qp_iter=qi)
+        infos = (OrcInfo * max(B, 1))()
+        li = None if lam_in is None else np.ascontiguousarray(lam_in, float).reshape(B, -1)
+        lo = np.zeros((B, N, nx + self.layout.nh)) if return_lam else None
+        qs = self.qp_mem_size()
+        qi_ = None if qp_in is None else np.ascontiguousarray(qp_in, float).reshape(B, qs)
+        qo = np.zeros((B, qs)) if return_qp else None
+        vp = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        self.L.orc_solve_batch_full(C.byref(self.pr), B, np.ascontiguousarray(params, float).reshape(-1),
+                                    np.ascontiguousarray(warm, float).reshape(-1),
+                                    np.ascontiguousarray(xinit, float).reshape(-1), vp(li), vp(qi_),
+                                    xt.reshape(-1), ut.reshape(-1), st, vp(lo), vp(qo),
+                                    C.cast(infos, C.c_void_p), nthreads)
+        get = lambda f, dt: np.array([getattr(infos[b], f) for b in range(B)], dt)  # noqa: E731
+        out = dict(xtraj=xt, utraj=ut, pobj=get("pobj", float), status=st, qp_iter=get("qp_iter_total", np.int32),
+                   sqp_iter=get("sqp_iter", np.int32), qp_status=get("qp_status", np.int32),
+                   res_eq=get("res_eq", float), res_stat=get("res_stat", float),
+                   res_ineq=get("res_ineq", float), res_comp=get("res_comp", float),
+                   qp_maxiter=get("qp_maxiter", np.int32))
+        if return_lam:
+            out["lam"] = lo
+        if return_qp:
+            out["qp"] = qo
+        return out

@@ -23,6 +23,22 @@ HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_confi
 BUILD = os.path.join(PKG, "build")
 
 
+def source_hash() -> str:
+    """sha256 over the HIP kernel sources, the C ABI header and the build flags: the identity of
+    the kernels a PMC profile was taken on (bench.py drops counters of other sources)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(list(SOURCES) + HEADERS):
+        h.update(f.encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(INCLUDE, "mpcg.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(repr((ARCH, sorted(SOURCES.items()))).encode())
+    return h.hexdigest()
+
+
 def _stale(target, deps):
     if not os.path.exists(target):
         return True

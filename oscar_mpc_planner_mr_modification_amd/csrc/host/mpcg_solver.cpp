@@ -3,6 +3,8 @@
 // (mpc_planner_solver/src/acados_solver_interface.cpp) method by method; the
 // acados capsule's persistent state (NLP iterate and multipliers, ocp_nlp_out)
 // is held here as `_iterate` / `_lam` and handed to the kernel on every solve.
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -121,8 +123,10 @@ void AcadosParameters::printParameters(const mpcg::YamlNode& parameter_map) cons
 }
 
 void Solver::AcadosInfo::print() const {
-    std::cout << "SQP iterations: " << sqp_iter << "\nQP iterations: " << qp_iter << "\nQP status: " << qp_status
-              << "\npobj: " << pobj << "\n";
+    // acados_solver_interface.h:111-122
+    std::cout << "SQP iterations: " << sqp_iter << "\nMinimum time for solve [ms]: " << min_time * 1000
+              << "\nKKT: " << kkt_norm_inf << "\nSolve Time [ms]: " << solvetime * 1000. << "\nNLP Residuals: " << nlp_res
+              << "\nQP iterations: " << qp_iter << "\nQP status: " << qp_status << "\npobj: " << pobj << "\n";
 }
 
 Solver::AcadosOutput::AcadosOutput() {
@@ -239,32 +243,45 @@ int Solver::run(int iterations) {
     }
     mpcg_context_set_iterations(_ctx, iterations);
     std::vector<double> xt((size_t)nx * (N + 1)), ut((size_t)nu * N), lam_out(_lam.size());
-    double pobj = 0.;
+    std::vector<double> qp_out((size_t)mpcg_qp_mem_size(&_problem));
+    double pobj = 0., stats[MPCG_STATS_STRIDE] = {0., 0., 0., 0.};
     int exit_code = 0, info[MPCG_INFO_STRIDE] = {0, 0, 0, 0};
     mpcg_io io{_params.all_parameters, _iterate.data(), _params.xinit, _lam.data(),
-               xt.data(), ut.data(), &pobj, &exit_code, info, lam_out.data()};
+               xt.data(), ut.data(), &pobj, &exit_code, info, lam_out.data(),
+               _qp.empty() ? nullptr : _qp.data(), qp_out.data(), stats};
+    const auto t0 = std::chrono::steady_clock::now();
     if (mpcg_context_solve(_ctx, 1, &io) != 0) {
         std::cerr << "[mpcg] solve failed: " << mpcg_last_error() << std::endl;
         _raw_status = 0;
         return 0;
     }
-    absorb(xt.data(), ut.data(), pobj, exit_code, info, lam_out.data());
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    absorb(xt.data(), ut.data(), pobj, exit_code, info, lam_out.data(), qp_out.data(), stats, sec);
     return exit_code;
 }
 
 void Solver::absorb(const double* xtraj, const double* utraj, double pobj, int exit_code, const int* info,
-                    const double* lam) {
+                    const double* lam, const double* qp, const double* stats, double seconds) {
     for (int k = 0; k <= N; ++k) {
         for (unsigned i = 0; i < nu; ++i) _iterate[k * nvar + i] = k < N ? utraj[k * nu + i] : 0.0;
         for (unsigned i = 0; i < nx; ++i) _iterate[k * nvar + nu + i] = xtraj[k * nx + i];
     }
     for (size_t i = 0; i < _lam.size(); ++i) _lam[i] = lam[i];
+    _qp.assign(qp, qp + mpcg_qp_mem_size(&_problem));
     _info.pobj = pobj;
     _info.sqp_iter += info[0];
     _info.qp_iter += info[1];
-    // acados QP status -> HPIPM status as explainExitFlag reads it
-    static const int hpipm[4] = {0, 3, 1, 2};
-    _info.qp_status = (info[2] >= 0 && info[2] < 4) ? hpipm[info[2]] : info[2];
+    _info.qp_status = info[2];  // the acados QP status, as ocp_nlp_get("qp_status") stores it (:157)
+    _info.res_stat = stats[0];
+    _info.res_eq = stats[1];
+    _info.res_ineq = stats[2];
+    _info.res_comp = stats[3];
+    _info.nlp_res = std::max(std::max(stats[0], stats[1]), std::max(stats[2], stats[3]));
+    _info.kkt_norm_inf = _info.nlp_res;
+    const double per_iter = seconds / std::max(1, info[0]);
+    _info.elapsed_time = per_iter;
+    _info.solvetime += seconds;
+    _info.min_time = std::min(_info.min_time, per_iter);
     _raw_status = exit_code;
 }
 
@@ -275,9 +292,11 @@ int Solver::completeOneIteration() {
         for (unsigned i = 0; i < nu; ++i) _output.utraj[k * nu + i] = _iterate[k * nvar + i];
     _exit_code_one_iter = _raw_status;  // res_eq rule and the 0 <-> 1 swap were applied by the kernel
     if (_exit_code_one_iter != 1) {
-        // Solver_acados_reset(capsule, 1): the capsule's iterate and multipliers go back to zero (:186-190)
+        // Solver_acados_reset(capsule, 1): the capsule's iterate and multipliers go back to zero, and
+        // ocp_nlp_solver_reset_qp_memory drops the QP warm start (:186-190)
         std::fill(_iterate.begin(), _iterate.end(), 0.0);
         std::fill(_lam.begin(), _lam.end(), 0.0);
+        _qp.clear();
     }
     return _exit_code_one_iter;
 }
@@ -450,12 +469,20 @@ std::vector<int> SolverBatch::solve(const std::vector<Solver*>& solvers) {
     _warm.resize(B * W);
     _xinit.resize(B * X);
     _lam_in.resize(B * L);
+    const size_t Q = (size_t)mpcg_qp_mem_size(&_problem);
     _xtraj.resize(B * XT);
     _utraj.resize(B * UT);
     _pobj.resize(B);
     _lam_out.resize(B * L);
+    _qp_in.resize(B * Q);
+    _qp_out.resize(B * Q);
+    _stats.resize((size_t)B * MPCG_STATS_STRIDE);
     _exit.resize(B);
     _info.resize((size_t)B * MPCG_INFO_STRIDE);
+    // the QP memory goes in as one block; a solver without one (fresh or reset) gets a block
+    // whose first value is NaN, which the kernel treats as absent (its first QP starts cold)
+    bool any_qp = false;
+    for (Solver* s : solvers) any_qp = any_qp || !s->_qp.empty();
     for (int b = 0; b < B; ++b) {
         Solver& s = *solvers[b];
         if (s.N != s0.N || s.npar != s0.npar || s._num_iterations != s0._num_iterations)
@@ -465,10 +492,14 @@ std::vector<int> SolverBatch::solve(const std::vector<Solver*>& solvers) {
         std::copy(s._iterate.begin(), s._iterate.end(), _warm.begin() + b * W);
         std::copy(s._params.xinit, s._params.xinit + X, _xinit.begin() + b * X);
         std::copy(s._lam.begin(), s._lam.end(), _lam_in.begin() + b * L);
+        if (!s._qp.empty()) std::copy(s._qp.begin(), s._qp.end(), _qp_in.begin() + b * Q);
+        else if (Q) _qp_in[b * Q] = std::nan("");
     }
     mpcg_context_set_iterations(_ctx, s0._num_iterations);
     mpcg_io io{_params.data(), _warm.data(), _xinit.data(), _lam_in.data(), _xtraj.data(), _utraj.data(),
-               _pobj.data(), _exit.data(), _info.data(), _lam_out.data()};
+               _pobj.data(), _exit.data(), _info.data(), _lam_out.data(), any_qp ? _qp_in.data() : nullptr,
+               _qp_out.data(), _stats.data()};
+    const auto t0 = std::chrono::steady_clock::now();
     if (mpcg_context_solve(_ctx, B, &io) != 0) {
         std::cerr << "[mpcg] batched solve failed: " << mpcg_last_error() << std::endl;
         for (int b = 0; b < B; ++b) {
@@ -477,10 +508,11 @@ std::vector<int> SolverBatch::solve(const std::vector<Solver*>& solvers) {
         }
         return codes;
     }
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (int b = 0; b < B; ++b) {
         Solver& s = *solvers[b];
         s.absorb(&_xtraj[b * XT], &_utraj[b * UT], _pobj[b], _exit[b], &_info[(size_t)b * MPCG_INFO_STRIDE],
-                 &_lam_out[b * L]);
+                 &_lam_out[b * L], &_qp_out[b * Q], &_stats[(size_t)b * MPCG_STATS_STRIDE], sec);
         codes[b] = s.completeOneIteration();
     }
     return codes;

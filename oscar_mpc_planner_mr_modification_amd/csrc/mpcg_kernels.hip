@@ -99,13 +99,17 @@ static int launch(const mpcg_problem& pr, int batch, const mpcg_io& io, hipStrea
 }
 
 using Fn = int (*)(const mpcg_problem&, int, const mpcg_io&, hipStream_t);
+struct Inst {
+    Fn fn = nullptr;
+    int qpm = 0;  // doubles of one solve's QP memory (Cfg::QPM)
+};
 
-static Fn find_instance(const mpcg_problem& pr) {
-    if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return nullptr;
-    if (pr.nu != (pr.model == MPCG_MODEL_BICYCLE_CA ? 3 : 2)) return nullptr;
+static Inst find_instance(const mpcg_problem& pr) {
+    if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return {};
+    if (pr.nu != (pr.model == MPCG_MODEL_BICYCLE_CA ? 3 : 2)) return {};
 #define MPCG_INST(N_, L_, E_, S_, X_, M_)                                                          \
     if (pr.model == M_ && pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_ && pr.n_scen == S_ && pr.nx == X_) \
-        return &launch<Cfg<N_, L_, E_, S_, X_, M_>>;
+        return {&launch<Cfg<N_, L_, E_, S_, X_, M_>>, Cfg<N_, L_, E_, S_, X_, M_>::QPM};
     MPCG_INST(20, 4, 4, 0, 5, 0)    // C1
     MPCG_INST(20, 8, 8, 0, 5, 0)    // C2 (north star)
     MPCG_INST(30, 12, 12, 0, 5, 0)  // C4
@@ -115,12 +119,12 @@ static Fn find_instance(const mpcg_problem& pr) {
     MPCG_INST(10, 0, 0, 4, 6, 0)
     MPCG_INST(10, 0, 0, 4, 6, 1)
 #undef MPCG_INST
-    return nullptr;
+    return {};
 }
 
 static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
     if (!pr || batch < 0) { g_err = "invalid arguments"; return -1; }
-    *fn = find_instance(*pr);
+    *fn = find_instance(*pr).fn;
     if (!*fn) {
         g_err = "no compiled instance for model=" + std::to_string(pr->model) + " N=" + std::to_string(pr->N) +
                 " nx=" + std::to_string(pr->nx) + " nu=" + std::to_string(pr->nu) +
@@ -139,11 +143,11 @@ struct mpcg_context {
     mpcg_problem pr;
     int max_batch = 0;
     hipStream_t stream = nullptr;
-    double* dev = nullptr;   // params | warm | xinit | lam_in | xtraj | utraj | pobj | lam_out
+    double* dev = nullptr;   // params | warm | xinit | lam_in | qp_in | xtraj | utraj | pobj | lam_out | qp_out | stats
     double* host = nullptr;  // pinned mirror of the same layout
     int* idev = nullptr;     // exit | info
     int* ihost = nullptr;
-    size_t n_par, n_warm, n_xi, n_lam, n_xt, n_ut, n_dbl, n_int;
+    size_t n_par, n_warm, n_xi, n_lam, n_qpm, n_xt, n_ut, n_st, n_dbl, n_int;
 };
 
 extern "C" {
@@ -155,7 +159,13 @@ void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps =
 
 const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }
 
-int mpcg_supported(const mpcg_problem* pr) { return (pr && mpcg::find_instance(*pr)) ? 0 : -1; }
+int mpcg_supported(const mpcg_problem* pr) { return (pr && mpcg::find_instance(*pr).fn) ? 0 : -1; }
+
+int mpcg_qp_mem_size(const mpcg_problem* pr) {
+    if (!pr) return -1;
+    const mpcg::Inst in = mpcg::find_instance(*pr);
+    return in.fn ? in.qpm : -1;
+}
 
 int mpcg_num_h(const mpcg_problem* pr) { return pr ? pr->n_lin + pr->n_ell + pr->n_scen : 0; }
 
@@ -261,6 +271,10 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->qp_mu0 = 1.0;
     pr->qp_thr0 = 1.0;
     pr->res_eq_fail = 1e-2;
+    // IPM start: cold (DESIGN.md §2 "QP start" -- the restated HPIPM warm start, qp_warm_start = 2 of
+    // generate_acados_solver.py:173, is available but breaks full-size GPU/oracle parity on C4 / C5)
+    pr->qp_warm_start = 0;
+    pr->qp_ws_thr = 0.1;
     return 0;
 }
 
@@ -296,9 +310,11 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
     c->n_warm = B * (N + 1) * (pr->nu + nx);
     c->n_xi = B * nx;
     c->n_lam = B * (size_t)mpcg_lam_size(pr);
+    c->n_qpm = B * (size_t)mpcg_qp_mem_size(pr);
     c->n_xt = B * (N + 1) * nx;
     c->n_ut = B * N * pr->nu;
-    c->n_dbl = c->n_par + c->n_warm + c->n_xi + 2 * c->n_lam + c->n_xt + c->n_ut + B;
+    c->n_st = B * MPCG_STATS_STRIDE;
+    c->n_dbl = c->n_par + c->n_warm + c->n_xi + 2 * c->n_lam + 2 * c->n_qpm + c->n_xt + c->n_ut + B + c->n_st;
     c->n_int = B * (1 + MPCG_INFO_STRIDE);
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&c->dev, c->n_dbl * sizeof(double)) == hipSuccess &&
@@ -340,28 +356,44 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
         return -1;
     }
     const mpcg_problem& pr = c->pr;
-    const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr);
+    const size_t B = batch, N = pr.N, L = (size_t)mpcg_lam_size(&pr), Q = (size_t)mpcg_qp_mem_size(&pr);
     const size_t nx = pr.nx;
     const size_t nu = pr.nu;
     const size_t s_par = B * N * pr.npar, s_warm = B * (N + 1) * (nu + nx), s_xi = B * nx, s_lam = B * L;
-    const size_t s_xt = B * (N + 1) * nx, s_ut = B * N * nu;
-    // inputs are packed contiguously (params | warm | xinit | lam_in) so one copy moves them
+    const size_t s_qpm = B * Q, s_xt = B * (N + 1) * nx, s_ut = B * N * nu, s_st = B * MPCG_STATS_STRIDE;
+    // inputs are packed contiguously (params | warm | xinit | lam_in | qp_in) so one copy moves them
     double* h = c->host;
     std::memcpy(h, io->params, s_par * sizeof(double));
     std::memcpy(h + s_par, io->warm, s_warm * sizeof(double));
     std::memcpy(h + s_par + s_warm, io->xinit, s_xi * sizeof(double));
     size_t n_in = s_par + s_warm + s_xi;
+    double* d = c->dev;
+    const double* d_lam = nullptr;
+    const double* d_qpi = nullptr;
     if (io->lam_in) {
         std::memcpy(h + n_in, io->lam_in, s_lam * sizeof(double));
+        d_lam = d + n_in;
         n_in += s_lam;
     }
-    double* d = c->dev;
-    double* d_out = d + c->n_par + c->n_warm + c->n_xi + c->n_lam;  // xtraj | utraj | pobj | lam_out
-    mpcg_io dio{d, d + s_par, d + s_par + s_warm, io->lam_in ? d + s_par + s_warm + s_xi : nullptr,
-                d_out, d_out + s_xt, d_out + s_xt + s_ut, c->idev, c->idev + B,
-                io->lam_out ? d_out + s_xt + s_ut + B : nullptr};
-    const size_t n_out = s_xt + s_ut + B + (io->lam_out ? s_lam : 0);
-    double* h_out = c->host + c->n_par + c->n_warm + c->n_xi + c->n_lam;
+    if (io->qp_in) {
+        std::memcpy(h + n_in, io->qp_in, s_qpm * sizeof(double));
+        d_qpi = d + n_in;
+        n_in += s_qpm;
+    }
+    // outputs: xtraj | utraj | pobj | lam_out | qp_out | stats, packed from the first output slot
+    const size_t o0 = c->n_par + c->n_warm + c->n_xi + c->n_lam + c->n_qpm;
+    double* d_out = d + o0;
+    double* h_out = c->host + o0;
+    size_t n_out = s_xt + s_ut + B;
+    double* d_lo = nullptr;
+    double* d_qo = nullptr;
+    double* d_st = nullptr;
+    size_t o_lo = 0, o_qo = 0, o_st = 0;
+    if (io->lam_out) { o_lo = n_out; d_lo = d_out + n_out; n_out += s_lam; }
+    if (io->qp_out) { o_qo = n_out; d_qo = d_out + n_out; n_out += s_qpm; }
+    if (io->stats) { o_st = n_out; d_st = d_out + n_out; n_out += s_st; }
+    mpcg_io dio{d, d + s_par, d + s_par + s_warm, d_lam, d_out, d_out + s_xt, d_out + s_xt + s_ut, c->idev,
+                c->idev + B, d_lo, d_qpi, d_qo, d_st};
     bool ok = hipMemcpyAsync(d, h, n_in * sizeof(double), hipMemcpyHostToDevice, c->stream) == hipSuccess;
     int rc = ok ? mpcg_solve(&pr, batch, &dio, c->stream) : -5;
     if (rc == 0)
@@ -377,7 +409,9 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
     std::memcpy(io->xtraj, h_out, s_xt * sizeof(double));
     std::memcpy(io->utraj, h_out + s_xt, s_ut * sizeof(double));
     std::memcpy(io->pobj, h_out + s_xt + s_ut, B * sizeof(double));
-    if (io->lam_out) std::memcpy(io->lam_out, h_out + s_xt + s_ut + B, s_lam * sizeof(double));
+    if (io->lam_out) std::memcpy(io->lam_out, h_out + o_lo, s_lam * sizeof(double));
+    if (io->qp_out) std::memcpy(io->qp_out, h_out + o_qo, s_qpm * sizeof(double));
+    if (io->stats) std::memcpy(io->stats, h_out + o_st, s_st * sizeof(double));
     std::memcpy(io->exit_code, c->ihost, B * sizeof(int));
     if (io->info) std::memcpy(io->info, c->ihost + B, B * MPCG_INFO_STRIDE * sizeof(int));
     return 0;

@@ -140,6 +140,11 @@ struct Cfg {
 #else
     static constexpr bool REC_FLAT = CHAIN_SPLIT && (PARTS == 3 || MPCG_REC_P2);
 #endif
+    // the capsule's QP memory (mpcg_io.qp_in / qp_out, opaque): per slot and lane the row's
+    // slack then multiplier ([2 s + {0, 1}][64 lanes]), then the QP step [N+1][NZ] and the
+    // dynamics multipliers [N][NX]
+    static constexpr int QPM_ROWS = 2 * SLOTS * 64;
+    static constexpr int QPM = QPM_ROWS + (N + 1) * NZ + N * NX;
     // slack coefficient of h row hh (scenario rows with the slack model)
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
@@ -508,12 +513,28 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     for (int e = lane; e < N * NX; e += 64)
         (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
     for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
+    // HPIPM warm start (qp_solver_warm_start 2): the QP memory of the capsule, if any, is the
+    // initial point of the first QP; the later QPs start from their predecessor's solution
+    const bool qp_warm = pr.qp_warm_start == 2;
+    bool have_qp = false;
+    if (qp_warm && io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
+        const double* q = io.qp_in + (size_t)sol * C::QPM;
+#pragma unroll
+        for (int sl = 0; sl < C::SLOTS; ++sl) {
+            R.t[sl] = q[(2 * sl) * 64 + lane];
+            R.l[sl] = q[(2 * sl + 1) * 64 + lane];
+        }
+        for (int e = lane; e < (N + 1) * NZ; e += 64) (&S.dz[0][0])[e] = q[C::QPM_ROWS + e];
+        for (int e = lane; e < N * NX; e += 64) (&S.piq[0][0])[e] = q[C::QPM_ROWS + (N + 1) * NZ + e];
+        have_qp = true;
+    }
     wave_sync();
     if (lane < NU) S.z[N][lane] = 0.0;
     wave_sync();
 
-    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0;
+    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0, n_maxit = 0;
     double res_eq = 0.0;
+    double nlp_stat = 0.0, nlp_ineq = 0.0, nlp_comp = 0.0;  // NLP residuals of the last linearisation
 
     for (int it = 0; it < pr.sqp_iters; ++it) {
         // parameter loads are re-issued where they are used rather than hoisted out of
@@ -654,6 +675,91 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
         // =============== feedback: QP by Riccati interior point ===============
         STAMP_BEGIN();
+        if (io.stats) {
+            // NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
+            // multipliers the NLP holds: pi_nlp and, per row, the previous QP's multiplier
+            // (FIXED_STEP: lam = lam_qp) or, before any QP, the carried h-row ones (box 0)
+            double rh[NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) rh[i] = 0.0;
+            double vin = 0.0, vcp = 0.0, vst = 0.0;
+#pragma unroll
+            for (int j = 0; j < BVS; ++j) {
+                double lb = 0.0;
+                if (LR.box_on(j)) {
+                    const double zv = S.z[k][LR.var(j)];
+                    const double gl = zv - LR.lo[j], gh = LR.hi[j] - zv;
+                    const double ll = have_qp ? R.l[2 * j] : 0.0, lh = have_qp ? R.l[2 * j + 1] : 0.0;
+                    vin = fmax(vin, -gl);
+                    vin = fmax(vin, -gh);
+                    vcp = fmax(vcp, fabs(ll * gl));
+                    vcp = fmax(vcp, fabs(lh * gh));
+                    lb = lh - ll;
+                }
+                if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = lb;
+            }
+#pragma unroll
+            for (int r = 0; r < HS; ++r) {
+                if (!LR.h_on(r)) continue;
+                const int hh = LR.hrow(r);
+                double a, bq, c;
+                rowg(hh, a, bq, c);
+                const double gap = rowgap(hh);
+                const double lam = have_qp ? R.l[HB + r] : R.nlam[r];
+                rh[0] += a * lam; rh[1] += bq * lam; rh[2] += c * lam;
+                if constexpr (NB == 4) rh[3] += C::slack_coef(hh) * lam;
+                vin = fmax(vin, -gap);
+                vcp = fmax(vcp, fabs(lam * gap));
+            }
+            double acc[NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) acc[i] = rh[i];
+#pragma unroll
+            for (int p = 1; p < PARTS; ++p)
+#pragma unroll
+                for (int i = 0; i < NB; ++i) acc[i] += lane_down(rh[i], p);
+            wave_sync();  // the owner lanes' box sums S.bx
+            if (stage_lane) {
+                double r[NZ];
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) r[i] = S.g[k][i] + S.bx[k][i];
+#pragma unroll
+                for (int i = 0; i < NB; ++i) r[C::bvar(i)] += acc[i];
+                if (k < N) {
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) {
+                        const double pm = S.pi_nlp[k][m];
+#pragma unroll
+                        for (int i = 0; i < NZ; ++i) r[i] += Fat(k, m, i) * pm;
+                    }
+                }
+                if (k > 0) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) r[NU + i] -= S.pi_nlp[k - 1][i];
+                }
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) {
+                    const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
+                    if (free_var) vst = fmax(vst, fabs(r[i]));
+                }
+            }
+            nlp_stat = wave_max(vst);
+            nlp_ineq = wave_max(vin);
+            nlp_comp = wave_max(vcp);
+            wave_sync();
+        }
+        if (qp_warm && have_qp) {
+            // HPIPM warm_start 2 (d_ocp_qp_ipm init_var): the previous QP's solution is the
+            // initial point -- step and dynamics multipliers stay in LDS, the rows' slacks and
+            // multipliers in registers -- with slacks and multipliers clipped below at thr0
+            const double thr = pr.qp_ws_thr;
+#pragma unroll
+            for (int sl = 0; sl < C::SLOTS; ++sl) {
+                if (R.t[sl] < thr) R.t[sl] = thr;
+                if (R.l[sl] < thr) R.l[sl] = thr;
+                R.pr[sl] = 0.0;
+            }
+        } else {
         // cold start: t = max(gap, thr0), l = mu0 / t
         {
             auto cold = [&](int s, double gap) {
@@ -687,6 +793,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < NX; ++i) S.piq[k][i] = 0.0;
             }
         }
+        }
+        have_qp = true;
         wave_sync();
         STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
@@ -1665,6 +1773,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         qp_status = qstat;
         qp_total += qit;
         ++sqp_iter;
+        n_maxit += qstat == AC_MAXITER;
         if (qstat != AC_SUCCESS && qstat != AC_MAXITER) {
             acados_status = AC_QP_FAILURE;
             break;
@@ -1715,6 +1824,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 if (LR.h_on(r)) lo[(size_t)k * LAMS + NX + LR.hrow(r)] = R.nlam[r];
         }
     }
+    if (io.qp_out) {
+        double* q = io.qp_out + (size_t)sol * C::QPM;
+#pragma unroll
+        for (int sl = 0; sl < C::SLOTS; ++sl) {
+            q[(2 * sl) * 64 + lane] = R.t[sl];
+            q[(2 * sl + 1) * 64 + lane] = R.l[sl];
+        }
+        for (int e = lane; e < (N + 1) * NZ; e += 64) q[C::QPM_ROWS + e] = (&S.dz[0][0])[e];
+        for (int e = lane; e < N * NX; e += 64) q[C::QPM_ROWS + (N + 1) * NZ + e] = (&S.piq[0][0])[e];
+    }
+    if (io.stats && lane == 0) {
+        double* st = io.stats + (size_t)sol * MPCG_STATS_STRIDE;
+        st[0] = nlp_stat;
+        st[1] = res_eq;
+        st[2] = nlp_ineq;
+        st[3] = nlp_comp;
+    }
     if (lane == 0) {
         int code = acados_status;
         if (res_eq > pr.res_eq_fail && code == AC_SUCCESS) code = AC_QP_FAILURE;
@@ -1726,7 +1852,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             io.info[(size_t)sol * MPCG_INFO_STRIDE + 0] = sqp_iter;
             io.info[(size_t)sol * MPCG_INFO_STRIDE + 1] = qp_total;
             io.info[(size_t)sol * MPCG_INFO_STRIDE + 2] = qp_status;
-            io.info[(size_t)sol * MPCG_INFO_STRIDE + 3] = 0;
+            io.info[(size_t)sol * MPCG_INFO_STRIDE + 3] = n_maxit;
         }
     }
     STAMP_STORE(stamps, sol);

@@ -44,20 +44,50 @@ def winner_records(xtraj, utraj, pobj, best, G, out=None):
     return out
 
 
-def gather_winners(records, world: int, out=None, group=None):
-    """All-gather of equally sized per-rank record blocks (one collective)."""
+def gather_winners(records, world: int, out=None, group=None, total: int | None = None):
+    """All-gather of the per-rank record blocks (one collective).
+
+    `total` is the number of scenes over all ranks, sharded by `shard()`. The
+    blocks may then differ in size (total % world != 0, or ranks without
+    scenes): every rank pads its block to ceil(total / world) rows, one
+    equal-size all-gather moves the padded blocks, and the real rows are
+    compacted in rank order.  Without `total` the blocks must all have
+    records.shape[0] rows (the bench's weak-scaling shards); `out` is then
+    the (world * rows, width) result buffer."""
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return records
-    if out is None:
-        out = torch.empty((records.shape[0] * world, records.shape[1]), dtype=records.dtype, device=records.device)
-    if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world, 0))
-        dist.all_gather(parts, records.contiguous(), group=group)
-        if parts[0].data_ptr() != out.data_ptr():
-            out.copy_(torch.cat(parts, 0))
+    width = records.shape[1]
+    if total is None:
+        per, counts = records.shape[0], None
     else:
-        dist.all_gather_into_tensor(out, records.contiguous(), group=group)
-    return out
+        per = -(-total // world)
+        counts = [shard(total, world, r)[1] for r in range(world)]
+        rank = dist.get_rank(group)
+        if records.shape[0] != counts[rank]:
+            raise ValueError(f"rank {rank} holds {records.shape[0]} records, its shard has {counts[rank]}")
+    if counts is None:
+        send = records.contiguous()
+        buf = out if out is not None else torch.empty((per * world, width), dtype=records.dtype,
+                                                      device=records.device)
+    else:
+        send = torch.zeros((per, width), dtype=records.dtype, device=records.device)
+        send[:records.shape[0]] = records
+        buf = torch.empty((per * world, width), dtype=records.dtype, device=records.device)
+    if dist.get_backend(group) == "gloo":
+        parts = list(buf.chunk(world, 0))
+        dist.all_gather(parts, send, group=group)
+        if parts[0].data_ptr() != buf.data_ptr():
+            buf.copy_(torch.cat(parts, 0))
+    else:
+        dist.all_gather_into_tensor(buf, send, group=group)
+    if counts is None:
+        return buf
+    blocks = [buf[r * per:r * per + counts[r]] for r in range(world)]
+    res = torch.cat(blocks, 0)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX,  # noqa: F401
+from .native_spec import (ABI_VERSION, DEFAULT_OPTIONS, EXPORTS, INFO_STRIDE, NU, NVAR, NX, STATS_STRIDE,  # noqa: F401
                           UNICYCLE_LB, UNICYCLE_UB, MpcgIo, MpcgProblem, MpcgSceneIo, MpcgStepIo, MpcgScenarioIo,
                           problem_from_layout)
 
@@ -37,6 +37,8 @@ def _load():
     lib.mpcg_supported.restype = C.c_int
     lib.mpcg_num_h.argtypes = [P]
     lib.mpcg_lam_size.argtypes = [P]
+    lib.mpcg_qp_mem_size.argtypes = [P]
+    lib.mpcg_qp_mem_size.restype = C.c_int
     lib.mpcg_problem_from_map.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_char_p),
                                           C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.c_double, C.c_int]
@@ -91,13 +93,22 @@ def lam_stride(pr: MpcgProblem) -> int:
     return pr.nx + pr.n_lin + pr.n_ell + pr.n_scen
 
 
+def qp_mem_size(pr: MpcgProblem) -> int:
+    """Doubles of one solve's QP memory (mpcg_io.qp_in / qp_out, opaque)."""
+    n = lib.mpcg_qp_mem_size(C.byref(pr))
+    if n < 0:
+        raise RuntimeError(f"mpcg_qp_mem_size: {last_error() or 'no compiled instance'}")
+    return n
+
+
 def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=None, lam_in=None,
-                       lam_out=False):
+                       lam_out=False, qp_in=None, qp_out=False, stats=False):
     """Batched solve on device tensors (torch, float64, on the current HIP device).
     params (B, N, npar), warm (B, N+1, nu+nx), xinit (B, nx), optional lam_in
-    (B, N, nx + nh) NLP multipliers carried over from the previous solve.
-    Returns a dict of device tensors (+ "lam" if lam_out); asynchronous on
-    `stream` (torch.cuda stream or None = current)."""
+    (B, N, nx + nh) NLP multipliers and qp_in (B, qp_mem_size) QP memory carried
+    over from the previous solve.  Returns a dict of device tensors (+ "lam" if
+    lam_out, "qp" if qp_out, "stats" (B, 4) NLP residuals if stats);
+    asynchronous on `stream` (torch.cuda stream or None = current)."""
     import torch
 
     B = params.shape[0]
@@ -118,12 +129,22 @@ def solve_batch_device(pr: MpcgProblem, params, warm, xinit, out=None, stream=No
                    info=torch.empty((B, INFO_STRIDE), dtype=torch.int32, device=dev))
     if lam_out and "lam" not in out:
         out["lam"] = torch.empty((B, N, LS), dtype=torch.float64, device=dev)
+    Q = qp_mem_size(pr) if (qp_in is not None or qp_out) else 0
+    if qp_in is not None:
+        assert tuple(qp_in.shape) == (B, Q) and qp_in.is_contiguous() and qp_in.dtype == torch.float64
+    if qp_out and "qp" not in out:
+        out["qp"] = torch.empty((B, Q), dtype=torch.float64, device=dev)
+    if stats and "stats" not in out:
+        out["stats"] = torch.empty((B, STATS_STRIDE), dtype=torch.float64, device=dev)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     io = MpcgIo(params.data_ptr(), warm.data_ptr(), xinit.data_ptr(),
                 None if lam_in is None else lam_in.data_ptr(),
                 out["xtraj"].data_ptr(), out["utraj"].data_ptr(), out["pobj"].data_ptr(), out["exit"].data_ptr(),
                 out["info"].data_ptr() if out.get("info") is not None else None,
-                out["lam"].data_ptr() if lam_out else None)
+                out["lam"].data_ptr() if lam_out else None,
+                None if qp_in is None else qp_in.data_ptr(),
+                out["qp"].data_ptr() if qp_out else None,
+                out["stats"].data_ptr() if stats else None)
     rc = lib.mpcg_solve(C.byref(pr), B, C.byref(io), C.c_void_p(s.cuda_stream))
     _check(rc, "mpcg_solve")
     return out
@@ -154,7 +175,7 @@ class Context:
     def set_iterations(self, sqp_iters: int):
         _check(lib.mpcg_context_set_iterations(self._c, sqp_iters), "mpcg_context_set_iterations")
 
-    def solve(self, params, warm, xinit, lam_in=None, lam_out=False):
+    def solve(self, params, warm, xinit, lam_in=None, lam_out=False, qp_in=None, qp_out=False, stats=False):
         pr = self.pr
         B, N, nx, NU = params.shape[0], pr.N, pr.nx, pr.nu
         LS = lam_stride(pr)
@@ -169,9 +190,16 @@ class Context:
             assert lam_in.shape == (B, N, LS)
         if lam_out:
             r["lam"] = np.zeros((B, N, LS))
+        if qp_in is not None:
+            qp_in = np.ascontiguousarray(qp_in, np.float64)
+            assert qp_in.shape == (B, qp_mem_size(pr))
+        if qp_out:
+            r["qp"] = np.zeros((B, qp_mem_size(pr)))
+        if stats:
+            r["stats"] = np.zeros((B, STATS_STRIDE))
         a = lambda x: None if x is None else x.ctypes.data  # noqa: E731
         io = MpcgIo(a(params), a(warm), a(xinit), a(lam_in), a(r["xtraj"]), a(r["utraj"]), a(r["pobj"]),
-                    a(r["exit"]), a(r["info"]), a(r.get("lam")))
+                    a(r["exit"]), a(r["info"]), a(r.get("lam")), a(qp_in), a(r.get("qp")), a(r.get("stats")))
         _check(lib.mpcg_context_solve(self._c, B, C.byref(io)), "mpcg_context_solve")
         return r
 

@@ -13,6 +13,7 @@ from .layouts import Layout
 NX, NU, NVAR = 5, 2, 7   # the T-MPC unicycle; the SH-MPC slack model has nx 6, the C3 bicycle nu 3 / nx 6
 MAX_NX, MAX_NU = 6, 3
 INFO_STRIDE = 4
+STATS_STRIDE = 4   # NLP residuals: stationarity, res_eq, inequality violation, complementarity
 
 
 class MpcgProblem(C.Structure):
@@ -35,11 +36,15 @@ class MpcgProblem(C.Structure):
         ("reg_eps", C.c_double), ("qp_mu0", C.c_double), ("qp_thr0", C.c_double),
         ("res_eq_fail", C.c_double),
         ("nu", C.c_int), ("model", C.c_int), ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int),
+        ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
     ]
 
 
-# acados options restated (generate_acados_solver.py:88-173) + our IPM cold start
-DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2)
+# acados options restated (generate_acados_solver.py:88-173: qp_tol, qp_solver_iter_max, MIRROR
+# epsilon) + the IPM's cold start; qp_warm_start=2 selects the restated HPIPM warm start
+# (qp_solver_warm_start, :173) with HPIPM's floor qp_ws_thr (DESIGN.md §2 "QP start")
+DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2,
+                       qp_warm_start=0, qp_ws_thr=0.1)
 # ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
 UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
 UNICYCLE_UB = (2.0, 0.8, 2000.0, 2000.0, 4 * np.pi, 3.0, 10000.0)
@@ -71,6 +76,8 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.qp_mu0 = o["qp_mu0"]
     pr.qp_thr0 = o["qp_thr0"]
     pr.res_eq_fail = o["res_eq_fail"]
+    pr.qp_warm_start = o["qp_warm_start"]
+    pr.qp_ws_thr = o["qp_ws_thr"]
     return pr
 
 
@@ -78,7 +85,8 @@ class MpcgIo(C.Structure):
     """Mirror of `mpcg_io` (include/mpcg.h)."""
     _fields_ = [("params", C.c_void_p), ("warm", C.c_void_p), ("xinit", C.c_void_p), ("lam_in", C.c_void_p),
                 ("xtraj", C.c_void_p), ("utraj", C.c_void_p), ("pobj", C.c_void_p),
-                ("exit_code", C.c_void_p), ("info", C.c_void_p), ("lam_out", C.c_void_p)]
+                ("exit_code", C.c_void_p), ("info", C.c_void_p), ("lam_out", C.c_void_p),
+                ("qp_in", C.c_void_p), ("qp_out", C.c_void_p), ("stats", C.c_void_p)]
 
 
 class MpcgSceneIo(C.Structure):
@@ -106,8 +114,8 @@ class MpcgScenarioIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
-ABI_VERSION = 4
-EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size",
+ABI_VERSION = 5
+EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size", "mpcg_qp_mem_size",
            "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
            "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device")

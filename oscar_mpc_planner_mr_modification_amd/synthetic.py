@@ -46,6 +46,17 @@ OBSTACLE_RADIUS = 0.325       # settings.yaml:43
 DECELERATION = 3.0            # settings.yaml:36 deceleration_at_infeasible
 CONTROL_PERIOD = 0.05         # settings.yaml:8 control_frequency 20 Hz
 SEED0 = 20251212
+# clearance of the synthetic guidance trajectories from every obstacle centre: robot
+# radius + obstacle radius (0.65, the ellipsoid rows' radius) + 0.25 m margin
+GUIDE_CLEAR = ROBOT_RADIUS + OBSTACLE_RADIUS + 0.25
+GUIDE_TRIES = 6
+# initial path heading range.  guidance_constraints.cpp:564 sets psi = atan2(vy, vx) of
+# the guidance velocity, which jumps by 2 pi where a guess crosses heading +-pi; the
+# first QP linearised across that jump is infeasible (scripts/qp_feasibility.py), a
+# reference behaviour the restated producer keeps.  The synthetic world frame is rotated
+# so that scenes do not sit on that cut (pi restores uniform headings).
+HEADING_SPAN = 0.5 * np.pi
+IMMINENT_S, IMMINENT_R = 1.0, 1.5   # obstacles reaching the robot's position this soon are redrawn
 
 
 @dataclass
@@ -69,7 +80,9 @@ def _path(rng, n_seg):
     coef = np.zeros((n_seg, 2, 4))
     starts = np.zeros(n_seg)
     px, py = rng.uniform(-5, 5), rng.uniform(-5, 5)
-    th = rng.uniform(-np.pi, np.pi)
+    # world frame: paths start heading within +-pi/2 of the x axis, away from the branch
+    # cut of the atan2 that initializeSolverWithGuidance uses for psi (see HEADING_SPAN)
+    th = rng.uniform(-HEADING_SPAN, HEADING_SPAN)
     s0 = 0.0
     for j in range(n_seg):
         L = rng.uniform(3.0, 6.0)
@@ -115,14 +128,51 @@ def _braking(x0, N, dt):
     return warm
 
 
+def _clear_path(pts, times, opos, ovel, dt, clear, sweeps=6):
+    """Push every sample of `pts` (at `times`) out to `clear` metres from each obstacle's
+    position at that time and one stage earlier (the prediction the solver's
+    constraints use at a stage, ellipsoid_constraints.cpp:66-70)."""
+    pts = pts.copy()
+    for _ in range(sweeps):
+        moved = False
+        for tk in (times - dt, times):
+            ob = opos[None, :, :] + ovel[None, :, :] * np.maximum(tk, 0.0)[:, None, None]  # (T, J, 2)
+            d = pts[:, None, :] - ob
+            dist = np.sqrt((d * d).sum(-1))
+            j = np.argmin(dist, 1)
+            dm = dist[np.arange(len(pts)), j]
+            bad = dm < clear
+            if bad.any():
+                moved = True
+                dv = d[np.arange(len(pts)), j] / np.maximum(dm, 1e-9)[:, None]
+                pts[bad] = ob[np.arange(len(pts)), j][bad] + dv[bad] * clear
+        if not moved:
+            break
+    return pts
+
+
+def _min_clearance(pos, opos, ovel, dt):
+    """smallest distance of the stage samples k = 1..N to the obstacles at t = (k-1) dt and k dt"""
+    N = len(pos) - 1
+    m = np.inf
+    for off in (1, 0):
+        t = (np.arange(1, N + 1) - off) * dt
+        ob = opos[None] + ovel[None] * t[:, None, None]
+        d = pos[1:, None, :] - ob
+        m = min(m, float(np.sqrt((d * d).sum(-1)).min()))
+    return m
+
+
 def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
-    """A collision-free guidance trajectory (stand-in for the external
-    guidance_planner's PRM output): nominal progress along the path at v_ref,
-    a lateral offset that passes obstacle j on side signs[j] (+1 left, -1
-    right) with clearance, then a radial push-out so that every sample keeps
-    `CLEAR` metres from every predicted obstacle position (the space-time
-    search of guidance_planner only returns collision-free paths).
-    Returns positions and velocities at t = k*dt, k = 0..N."""
+    """A collision-free, kinematically consistent guidance trajectory (stand-in for the
+    external guidance_planner's space-time PRM output): nominal progress along the
+    path towards v_ref, a lateral offset that passes obstacle j on side signs[j]
+    (+1 left, -1 right), the desired path pushed out to a clearance from every
+    obstacle in space-time, then tracked by a pure-pursuit unicycle inside the input
+    bounds from the current state (guidance_planner's search starts from the robot's
+    state and only returns collision-free trajectories).
+    Returns positions and velocities at t = k*dt, k = 0..N, and the smallest clearance
+    of the stage samples from the obstacles (the constraints' and the physical time)."""
     coef, starts, s_ego = tangent_path
     CLEAR = 0.8
     fine = np.linspace(0, N * dt, 8 * N + 1)
@@ -144,6 +194,10 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
         off += want * np.exp(-0.5 * ((fine - fine[ic]) / 1.2) ** 2) * (1.0 - np.exp(-fine / 0.8))
     desired = nom + off[:, None] * nrm
     desired = desired - desired[0] + ego[:2]
+    if obstacles:
+        opos = np.array([o[0] for o in obstacles])
+        ovel = np.array([o[1] for o in obstacles])
+        desired = _clear_path(desired, fine, opos, ovel, dt, GUIDE_CLEAR + 0.3)
     # track the desired path with a pure-pursuit unicycle inside the input
     # bounds (|a| <= 2, |w| <= 0.8), so the guess is kinematically reachable
     # from the current state, as guidance_planner's start-state-aware search is
@@ -169,7 +223,9 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
         v = max(v + h * a, 0.0)
     vel = np.gradient(traj, fine, axis=0)
     idx = np.searchsorted(fine, np.arange(N + 1) * dt - 1e-12)
-    return traj[idx], vel[idx]
+    pos = traj[idx]
+    clear = _min_clearance(pos, opos, ovel, dt) if obstacles else np.inf
+    return pos, vel[idx], clear
 
 
 def make_scenes(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | None = None,
@@ -206,11 +262,19 @@ def make_scenes(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | 
         state[sc] = x0
         obstacles = []
         for j in range(n_obs):
-            ahead = rng.uniform(2.0, 10.0)
-            lat = rng.uniform(-3.0, 3.0)
-            pj, tj = _path_eval(coef, starts, s_ego + ahead)
-            nj = np.array([-tj[1], tj[0]])
-            obstacles.append((pj + lat * nj, rng.normal(0.0, 0.7, size=2)))
+            # an obstacle on a collision course with the robot's current position inside
+            # the first second is redrawn (the scene would start in an unavoidable
+            # collision, which the reference's planner never faces in steady operation)
+            for _ in range(20):
+                ahead = rng.uniform(2.0, 10.0)
+                lat = rng.uniform(-3.0, 3.0)
+                pj, tj = _path_eval(coef, starts, s_ego + ahead)
+                nj = np.array([-tj[1], tj[0]])
+                op, ov = pj + lat * nj, rng.normal(0.0, 0.7, size=2)
+                tt = np.linspace(0.0, IMMINENT_S, 11)
+                if np.min(np.linalg.norm(op[None] + ov[None] * tt[:, None] - ego_pos[None], axis=1)) >= IMMINENT_R:
+                    break
+            obstacles.append((op, ov))
         # stage-invariant module parameters (mpc_base.cpp:23-35, contouring.cpp:52-126,
         # ellipsoid_constraints.cpp:38-40)
         base = stage_params[sc]
@@ -250,12 +314,23 @@ def make_scenes(layout: Layout, n_scenes: int, n_guesses: int = 8, n_obs: int | 
                 prev_sel[sc, sel] = True
         for g in range(G - 1):
             signs = [1 if (g >> (j % 3)) & 1 else -1 for j in range(n_obs)]
+            grng = np.random.default_rng(seed + 7919 * ((first_scene + sc) * G + g))
             if g >= 8:
-                signs = list(np.random.default_rng(seed + 7919 * ((first_scene + sc) * G + g)).choice([-1, 1], n_obs))
-            pos, vel = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
-                                         SETTINGS_WEIGHTS["reference_velocity"])
-            guidance[sc, g, :, 0:2] = pos
-            guidance[sc, g, :, 2:4] = vel
+                signs = list(grng.choice([-1, 1], n_obs))
+            # guidance_planner returns only collision-free homotopies: a passing pattern
+            # whose tracked trajectory cannot keep the clearance is replaced by another
+            # one (random side per obstacle), the best of GUIDE_TRIES kept otherwise
+            best = None
+            for _ in range(GUIDE_TRIES):
+                pos, vel, clear = _guess_trajectory(x0, (coef, starts, s_ego), obstacles, signs, N, dt,
+                                                    SETTINGS_WEIGHTS["reference_velocity"])
+                if best is None or clear > best[2]:
+                    best = (pos, vel, clear)
+                if clear >= GUIDE_CLEAR:
+                    break
+                signs = list(grng.choice([-1, 1], n_obs))
+            guidance[sc, g, :, 0:2] = best[0]
+            guidance[sc, g, :, 2:4] = best[1]
     return Scenes(stage_params=stage_params, state=state, obst=obst, obst_meta=meta, guidance=guidance,
                   guided=guided, prev_traj=prev, prev_elapsed=elapsed, consistency_on=cons_on,
                   previously_selected=prev_sel, main_warm=None)

@@ -1,0 +1,74 @@
+"""Workload diagnostics (CPU, oracle): success fraction, executed RTI iterations and
+IPM iterations of the bench's synthetic solves, and how often the guided warm starts
+violate their own topology halfspaces / the obstacle ellipsoids.
+
+    python scripts/diag_workload.py [--config C2] [--scenes 64] [--ws 0|2]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+
+
+def warm_violations(lay, b):
+    """fraction of solves whose warm start violates a halfspace / an ellipsoid at some stage 1..N-1"""
+    N = lay.N
+    P, W = b.params, b.warm
+    x, y = W[:, 1:N, 2], W[:, 1:N, 3]
+    hv = np.zeros(len(P), bool)
+    if lay.n_lin:
+        l0 = lay.idx("lin_constraint_0_a1")
+        c = P[:, 1:N, l0:l0 + 3 * lay.n_lin].reshape(len(P), N - 1, lay.n_lin, 3)
+        h = c[..., 0] * x[..., None] + c[..., 1] * y[..., None] - c[..., 2]
+        hv = (h > 1e-9).any(axis=(1, 2))
+    ev = np.zeros(len(P), bool)
+    if lay.n_ell:
+        e0 = lay.idx("ellipsoid_obst_0_x")
+        o = P[:, 1:N, e0:e0 + 7 * lay.n_ell].reshape(len(P), N - 1, lay.n_ell, 7)
+        r = o[..., 6] + P[:, 1:N, lay.idx("ego_disc_radius")][..., None]
+        d = np.hypot(x[..., None] - o[..., 0], y[..., None] - o[..., 1])
+        ev = (d < r).any(axis=(1, 2))
+    return hv, ev
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--scenes", type=int, default=64)
+    ap.add_argument("--ws", type=int, default=2)
+    ap.add_argument("--first", type=int, default=0)
+    args = ap.parse_args()
+    import oracle_py
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+    lay = config_layout(args.config)
+    t0 = time.time()
+    b = make_batch(lay, args.scenes, 8, first_scene=args.first, workers=8)
+    tg = time.time() - t0
+    orc = oracle_py.Oracle(lay, qp_warm_start=args.ws)
+    t0 = time.time()
+    r = orc.solve_batch(b.params, b.warm, b.xinit)
+    ts = time.time() - t0
+    ok = r["status"] == 1
+    hv, ev = warm_violations(lay, b)
+    g = b.guided
+    print(f"{args.config} {len(ok)} solves (gen {tg:.1f}s, solve {ts:.1f}s) ws={args.ws}")
+    print(f"  success {ok.mean():.3f} (guided {ok[g].mean():.3f}, non-guided {ok[~g].mean():.3f})")
+    print(f"  rti iters/solve {r['sqp_iter'].mean():.2f}  qp iters/solve {r['qp_iter'].mean():.1f}  "
+          f"qp iters/rti {r['qp_iter'].sum() / r['sqp_iter'].sum():.2f}")
+    print(f"  one-iteration exits {(r['sqp_iter'] == 1).mean():.3f}; status counts {np.bincount(r['status'], minlength=5)}")
+    print(f"  last qp status counts {np.bincount(r['qp_status'], minlength=4)}")
+    print(f"  guided warm starts violating halfspaces {hv[g].mean():.3f} (failing {hv[g & ~ok].mean() if (g & ~ok).any() else 0:.3f}),"
+          f" ellipsoids {ev[g].mean():.3f} (failing {ev[g & ~ok].mean() if (g & ~ok).any() else 0:.3f})")
+    sc_ok = ok.reshape(-1, 8).any(1)
+    print(f"  scenes with a feasible planner {sc_ok.mean():.3f}")
+
+
+if __name__ == "__main__":
+    main()

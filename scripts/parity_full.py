@@ -1,0 +1,95 @@
+"""Full-size GPU-vs-oracle parity of the bench batches (GPU box).
+
+    python scripts/parity_full.py [--configs C2,C4,C5] [--ws 2] [--scenes N]
+
+For each config: the bench's synthetic inputs, one batched GPU solve, the C oracle
+on the same inputs (OpenMP), then exit agreement, max |x - x_ref| over successful
+and over failed solves, and the indices of disagreeing solves (JSON on stdout).
+Test infrastructure: imports the oracle."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+
+DEFAULT_SCENES = {"C2": 1024, "C4": 2048, "C5": 2048, "C3": 4096, "C1": 1024}
+
+
+def inputs(cfg, S, first=0):
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    lay = config_layout(cfg)
+    if cfg == "C5":
+        from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_batch
+        b = make_shmpc_batch(lay, S, first_scene=first)
+    elif cfg == "C3":
+        from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch
+        b = make_c3_batch(lay, S, first_scene=first)
+    else:
+        from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+        b = make_batch(lay, S, 8 if cfg != "C1" else 1, first_scene=first, workers=16)
+    return lay, b
+
+
+def compare(cfg, S, ws, first=0):
+    import torch
+
+    import oracle_py
+    from oscar_mpc_planner_mr_modification_amd import native
+
+    lay, b = inputs(cfg, S, first)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pr = native.problem_from_layout(lay, qp_warm_start=ws)
+    out = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), stats=True)
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    t0 = time.time()
+    ref = oracle_py.Oracle(lay, qp_warm_start=ws).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
+    t_orc = time.time() - t0
+    same = got["exit"] == ref["status"]
+    ok = same & (got["exit"] == 1)
+    bad = same & (got["exit"] != 1)
+    dx = np.abs(got["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
+    st = np.stack([ref["res_stat"], ref["res_eq"], ref["res_ineq"], ref["res_comp"]], 1)
+    st_rel = (np.abs(got["stats"] - st) / np.maximum(1.0, np.abs(st)))[same].max() if same.any() else 0.0
+    dis = np.flatnonzero(~same)
+    # failed solves that took the same path on both sides (same RTI and IPM iteration counts) with
+    # every accepted step from a converged QP
+    path = (bad & (got["info"][:, 0] == ref["sqp_iter"]) & (got["info"][:, 1] == ref["qp_iter"]) &
+            (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0))
+    return {"config": cfg, "qp_warm_start": ws, "solves": int(len(same)), "exit_agreement": float(same.mean()),
+            "success_frac": float((ref["status"] == 1).mean()), "rti_iters_per_solve": float(ref["sqp_iter"].mean()),
+            "qp_iters_per_solve_gpu": float(got["info"][:, 1].mean()), "qp_iters_per_solve_oracle": float(ref["qp_iter"].mean()),
+            "max_abs_dx_success": float(dx[ok].max()) if ok.any() else None,
+            "max_abs_dx_failed": float(dx[bad].max()) if bad.any() else None,
+            "failed_dx_over_1e-4": int((dx[bad] > 1e-4).sum()),
+            "same_path_failed": int(path.sum()),
+            "maxiter_qp_solves_gpu": int((got["info"][:, 3] > 0).sum()),
+            "maxiter_info_agreement": float((got["info"][:, 3] == ref["qp_maxiter"]).mean()),
+            "same_path_failed_dx": float(dx[path].max()) if path.any() else None,
+            "stats_max_rel_diff": float(st_rel),
+            "disagreeing": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
+                             "gpu_info": got["info"][i].tolist(), "oracle_sqp": int(ref["sqp_iter"][i]),
+                             "oracle_qp_status": int(ref["qp_status"][i])} for i in dis[:20]],
+            "oracle_s": round(t_orc, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C4,C5")
+    ap.add_argument("--ws", default="2")
+    ap.add_argument("--scenes", type=int, default=None)
+    args = ap.parse_args()
+    for cfg in args.configs.split(","):
+        for ws in (int(w) for w in args.ws.split(",")):
+            r = compare(cfg, args.scenes or DEFAULT_SCENES[cfg], ws)
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -97,7 +97,10 @@ def main():
     json.dump(res, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
     sq = res["kernels"].get("sqp_kernel", {})
     if "hbm_bytes_per_launch" in sq:
-        tr = {"tag": tag, "config": args.config, "batch": args.batch,
+        import sys
+        sys.path.insert(0, ROOT)
+        from oscar_mpc_planner_mr_modification_amd._build import source_hash
+        tr = {"tag": tag, "config": args.config, "batch": args.batch, "source_sha256": source_hash(),
               "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
               "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"],
               "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch")}

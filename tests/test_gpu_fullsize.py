@@ -1,0 +1,41 @@
+"""Full-size GPU-vs-oracle parity on the bench batches (BASELINE.json configs):
+C2 1024 scenes x 8 guesses, C4 2048 x 8 (one GPU's shard of 16384), C5 2048 x 4
+parallel scenario solvers.  Exit codes identical on every solve, trajectories of
+successful solves within 1e-4, and failed solves that took the same path (same
+RTI and interior-point iteration counts on both sides) also within 1e-4.
+
+C5 exception: the SH-MPC slack state is pinned at 0 by the x0
+bound and its zero dynamics (generate_acados_solver.py:95, solver_model.py:289-292),
+so its lower-bound rows have zero gap at every stage.  On a few QPs the interior
+point stalls on the central path and the Riccati pivot's sign is then decided by
+rounding; such a solve ends in a QP NaN status on one side.  The test bounds their
+number and checks that every disagreement is of that kind."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["C2", "C4", "C5"])
+def test_fullsize_exit_agreement(cfg):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from parity_full import DEFAULT_SCENES, compare
+
+    r = compare(cfg, DEFAULT_SCENES[cfg], 0)
+    print(r)
+    assert r["max_abs_dx_success"] <= 1e-4
+    assert r["same_path_failed_dx"] is None or r["same_path_failed_dx"] <= 1e-4
+    if cfg in ("C2", "C4"):
+        assert r["exit_agreement"] == 1.0
+        assert r["success_frac"] >= 0.9, r["success_frac"]
+        assert r["rti_iters_per_solve"] >= 9.0
+    else:
+        assert r["exit_agreement"] >= 0.999
+        for d in r["disagreeing"]:
+            assert d["gpu_info"][2] == 1 or d["oracle_qp_status"] == 1, d
