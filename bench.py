@@ -31,6 +31,8 @@ scenes per GPU, N=30, CA spline update, CA contouring and 12 decomp
 halfspaces per stage, one solver per scene.
 `--config C4`: N=30, 12 obstacles, 2048 scenes x 8 guesses per GPU (one GPU's
 shard of BASELINE.json configs[3]).
+`--config JS`: the reference's shipped jackalsimulator solver (N=30, 4 obstacles,
+4 guided + 1 non-guided planners), 4096 scenes x 5 planners per GPU.
 `--config C5`: SH-MPC, 2048 scenes x 4 parallel scenario solvers per GPU on the
 slack model, 24 scenario halfspaces per stage reduced on the GPU from 12
 obstacles x 100 prediction samples (mpcg_prepare_scenario), batched solve,
@@ -50,7 +52,8 @@ sys.path.insert(0, ROOT)
 METRIC = "SQP solves/s (N=20, 8 obs, 8 guesses) at 1/2/4/8 MI355X; max |x−x_ref|"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (vendor spec)
-DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048}
+DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048, "JS": 4096}
+DEFAULT_GUESSES = {"JS": 5}    # jackalsimulator as shipped: n_paths 4 + the non-guided planner
 CHECK_CHUNK = 256              # solves per oracle call in the check leg
 RANK_SAMPLE = 256              # solves each rank checks at N > 1
 
@@ -101,7 +104,7 @@ class Workload:
 
 
 class TmpcWorkload(Workload):
-    """C1 / C2 / C4: T-MPC++ control step (prepare -> solve -> select -> winner records)."""
+    """C1 / C2 / C4 / JS: T-MPC++ control step (prepare -> solve -> select -> winner records)."""
     phases = ("prepare", "solve")
 
     def __init__(self, args, lay, rank, world, dev):
@@ -344,13 +347,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=sorted(DEFAULT_SCENES))
     ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2: 1024, C3: 4096, C4: 2048, C5: 2048)")
-    ap.add_argument("--guesses", type=int, default=8)
+    ap.add_argument("--guesses", type=int, default=None, help="planners per scene (8; JS: 5)")
     ap.add_argument("--qp-warm-start", type=int, default=0, choices=(0, 2),
                     help="IPM start: 0 cold (default), 2 the restated HPIPM warm start (DESIGN.md §2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle (CPU baseline and parity)")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default profiles/traffic_<config>.json)")
     args = ap.parse_args()
+    if args.guesses is None:
+        args.guesses = DEFAULT_GUESSES.get(args.config, 8)
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
 

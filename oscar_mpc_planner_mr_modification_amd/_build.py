@@ -15,8 +15,11 @@ ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 
 # source -> extra flags.  The producers are compiled without floating-point
 # contraction so that they agree bit for bit with the host restatement.
-SOURCES = {"mpcg_kernels.hip": [], "mpcg_prepare.hip": ["-ffp-contract=off"]}
-HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h", "mpcg_bicycle.h"]
+SOURCES = {"mpcg_kernels.hip": [], "mpcg_prepare.hip": ["-ffp-contract=off"],
+           # built-in kernel instances, one translation unit per family (compiled in parallel)
+           "mpcg_inst_tmpc20.hip": [], "mpcg_inst_tmpc30.hip": [], "mpcg_inst_shmpc.hip": [],
+           "mpcg_inst_bicycle.hip": []}
+HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h", "mpcg_bicycle.h", "mpcg_instance.h"]
 HOST_SOURCES = ["host/mpcg_yaml.cpp", "host/mpcg_solver.cpp"]
 HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_config.h", "mpc_planner_solver/state.h",
                 "mpc_planner_solver/mpcg_solver_interface.h", "mpc_planner_solver/solver_interface.h"]
@@ -65,7 +68,7 @@ def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: s
     for p in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, "hipcc")
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-soname,libmpcg.so", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -73,25 +76,68 @@ def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: s
     return out
 
 
-def build_cpp(config: str = "C2", force: bool = False, verbose: bool = False) -> dict:
+def _hipcc_obj(src, obj, extra=()):
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}",
+           *extra, "-c", src, "-o", obj]
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def build_instance(layout, out_dir: str, force: bool = False) -> str:
+    """libmpcg_inst_<name>.so: the kernel instance of `layout`'s dimensions (codegen
+    mpcg_instance.hip) as a library that registers itself with libmpcg.so on load
+    (native.load_instances)."""
+    from . import codegen
+
+    lib_mpcg = build_lib()
+    os.makedirs(out_dir, exist_ok=True)
+    src = os.path.join(out_dir, "mpcg_instance.hip")
+    text = codegen.instance_source(layout)
+    if not os.path.exists(src) or open(src).read() != text:
+        with open(src, "w") as fh:
+            fh.write(text)
+    so = os.path.join(out_dir, f"libmpcg_inst_{layout.name}.so")
+    deps = [src, lib_mpcg] + [os.path.join(CSRC, h) for h in HEADERS]
+    if force or _stale(so, deps):
+        obj = _hipcc_obj(src, os.path.join(out_dir, "mpcg_instance.o"))
+        subprocess.run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so + ".tmp", obj, f"-L{PKG}",
+                        "-lmpcg", f"-Wl,-rpath,{PKG}"], check=True)
+        os.replace(so + ".tmp", so)
+    return so
+
+
+def build_cpp(config="C2", force: bool = False, verbose: bool = False) -> dict:
     """The drop-in C++ MPCPlanner::Solver for one generated solver
     (dimensions are compile-time, as in the reference): codegen into
-    build/<config>/, then libmpc_planner_solver.so and the test program
-    tests/cpp/test_solver.cpp linked against libmpcg.so."""
+    build/<name>/, then libmpc_planner_solver.so -- the host sources plus the
+    generated kernel instance of these dimensions -- and the test program
+    tests/cpp/test_solver.cpp, linked against libmpcg.so.  `config` is a
+    config name or a Layout."""
     from . import codegen
     from .layouts import config_layout
 
+    lay = config_layout(config) if isinstance(config, str) else config
     lib_mpcg = build_lib()
-    out = os.path.join(BUILD, config)
-    codegen.generate(config_layout(config), out)
+    out = os.path.join(BUILD, lay.name)
+    codegen.generate(lay, out)
     so = os.path.join(out, "libmpc_planner_solver.so")
     exe = os.path.join(out, "test_solver")
     srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES] + [os.path.join(out, "mpc_planner_parameters.cpp")]
-    deps = srcs + [os.path.join(INCLUDE, h) for h in HOST_HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), lib_mpcg,
-                                                                     __file__]
+    inst = os.path.join(out, "mpcg_instance.hip")
+    deps = srcs + [inst] + [os.path.join(INCLUDE, h) for h in HOST_HEADERS] + \
+        [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), lib_mpcg, __file__]
     inc = [f"-I{os.path.join(out, 'include')}", f"-I{INCLUDE}"]
     if force or _stale(so, deps):
-        cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra"] + inc + srcs + \
+        objs = []
+        for src in srcs:
+            obj = os.path.join(out, os.path.basename(src).replace(".cpp", ".o"))
+            cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra"] + inc + ["-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+            objs.append(obj)
+        objs.append(_hipcc_obj(inst, os.path.join(out, "mpcg_instance.o")))
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + \
               ["-o", so + ".tmp", f"-L{PKG}", "-lmpcg", f"-Wl,-rpath,{PKG}"]
         if verbose:
             print(" ".join(cmd))

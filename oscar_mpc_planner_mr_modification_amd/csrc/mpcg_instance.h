@@ -1,0 +1,50 @@
+// mpcg_instance.h — compiled kernel instances of the batched SQP solve.
+//
+// The kernel is specialised at compile time on the generated solver's dimensions, as
+// the reference's acados / Forces solvers are generated per configuration
+// (solver_generator/generate_solver.py).  An instance is one Cfg<N, n_lin, n_ell,
+// n_scen, nx, model>; it registers its launcher with libmpcg.so's instance table from a
+// static initialiser, so a translation unit with MPCG_DEFINE_INSTANCE(...) adds a
+// shape to any process that loads it: the built-in instances (mpcg_inst_*.hip in
+// libmpcg.so) and the one codegen.py writes for a generated solver directory
+// (mpcg_instance.hip, compiled into the drop-in libmpc_planner_solver.so).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcg.h"
+#include "mpcg_sqp.h"
+
+extern "C" {
+/* launcher of one compiled instance: enqueues the solve of `batch` problems on `stream`
+ * and returns the hipError_t of the launch */
+typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream,
+                                    unsigned long long* stamps);
+/* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher and the
+ * doubles of one solve's QP memory.  Returns 0 (a shape already present keeps its first
+ * launcher). */
+int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
+                           int qp_mem_size);
+}
+
+namespace mpcg {
+
+template <class C>
+int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps) {
+    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync)
+    hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io, stamps);
+    return (int)hipGetLastError();
+}
+
+template <class C>
+int register_instance() {
+    return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM);
+}
+
+}  // namespace mpcg
+
+#define MPCG_INST_CAT2(a, b) a##b
+#define MPCG_INST_CAT(a, b) MPCG_INST_CAT2(a, b)
+// one instance: Cfg<N, n_lin, n_ell, n_scen, nx, model>
+#define MPCG_DEFINE_INSTANCE(N_, L_, E_, S_, X_, M_)                                                  \
+    static const int MPCG_INST_CAT(mpcg_instance_reg_, __COUNTER__) =                                \
+        mpcg::register_instance<mpcg::Cfg<N_, L_, E_, S_, X_, M_>>();

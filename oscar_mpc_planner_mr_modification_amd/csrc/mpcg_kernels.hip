@@ -1,31 +1,27 @@
-// mpcg_kernels.hip — MI355X (gfx950) kernels of the batched T-MPC++ SQP solve.
+// mpcg_kernels.hip — the C ABI of the MI355X (gfx950) batched T-MPC++ SQP solve
+// (include/mpcg.h): problem description from a parameter map, dispatch to the compiled
+// kernel instances (mpcg_instance.h; the built-in ones live in mpcg_inst_*.hip), the
+// persistent host-buffer context, and the per-scene selection kernels.
 //
-// One wavefront (64 lanes, one workgroup) solves one (scene, guess) pair:
-// the body of one `Solver::solve()` call of the OpenMP fan-out in
-// GuidanceConstraints::optimize (guidance_constraints.cpp:304-421), i.e.
-// `sqp_iters` acados SQP-RTI iterations (acados_solver_interface.cpp:86-119).
-//
-// Lane roles inside the wave
-//   * stage lanes   lane k in [0, N]: linearisation of shooting stage k (cost,
-//                   ERK4 sensitivities + exact Hessian, constraints, MIRROR),
-//                   and every per-inequality interior-point operation of stage k
-//   * element lanes lane e < nz (nz + 1) / 2: one entry (i >= j) of the Riccati stage
-//                   block during the backward factorisation
-//   * all lanes     redundant scalar recursions (vector pass, forward pass),
-//                   so no LDS round trip sits on those sequential chains
-// All QP data of one solve lives in LDS (struct Lds below); stage-indexed
-// arrays are stage-minor so stage lanes access consecutive 8-byte words.
-// Reductions (max residual, complementarity sum, step length) are xor
-// butterflies: bit-identical in every lane, deterministic.
+// The solve kernel itself is sqp_kernel<Cfg<...>> in mpcg_sqp.h: one wavefront (64
+// lanes, one workgroup) solves one (scene, guess) pair -- the body of one
+// `Solver::solve()` call of the OpenMP fan-out in GuidanceConstraints::optimize
+// (guidance_constraints.cpp:304-421), i.e. `sqp_iters` acados SQP-RTI iterations
+// (acados_solver_interface.cpp:86-119).  Its lanes are stage x part (stage algebra,
+// inequality rows), element lanes of the Riccati block, and vector chains carried in
+// SGPRs; inequality-row state lives in registers, stage blocks in LDS; reductions are
+// DPP trees read back from lane 63 (see the header of mpcg_sqp.h and DESIGN.md §3).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "mpcg.h"
 #include "mpcg_device.h"
-#include "mpcg_sqp.h"
+#include "mpcg_instance.h"
 
 namespace mpcg {
 
@@ -86,40 +82,42 @@ __global__ void select_lowest_cost_kernel(int n_scenes, int P, const double* __r
 thread_local std::string g_err;  // also set by mpcg_prepare.hip
 static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG_STAMPS builds only)
 
-template <class C>
-static int launch(const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream) {
-    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync)
-    hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, stream, pr, batch, io, g_stamps);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        g_err = std::string("sqp_kernel launch: ") + hipGetErrorString(e);
-        return -1;
-    }
-    return 0;
-}
-
-using Fn = int (*)(const mpcg_problem&, int, const mpcg_io&, hipStream_t);
+// the instance table (mpcg_instance.h): built-in instances register from mpcg_inst_*.hip,
+// generated solvers from the drop-in library codegen.py writes
 struct Inst {
-    Fn fn = nullptr;
+    int model = 0, N = 0, nl = 0, ne = 0, ns = 0, nx = 0;
+    mpcg_instance_launch fn = nullptr;
     int qpm = 0;  // doubles of one solve's QP memory (Cfg::QPM)
 };
+static std::mutex& registry_mutex() {
+    static std::mutex m;
+    return m;
+}
+static std::vector<Inst>& registry() {
+    static std::vector<Inst> r;
+    return r;
+}
 
 static Inst find_instance(const mpcg_problem& pr) {
     if (pr.rk_steps < 1 || pr.n_seg < 1 || pr.n_seg > 16) return {};
     if (pr.nu != (pr.model == MPCG_MODEL_BICYCLE_CA ? 3 : 2)) return {};
-#define MPCG_INST(N_, L_, E_, S_, X_, M_)                                                          \
-    if (pr.model == M_ && pr.N == N_ && pr.n_lin == L_ && pr.n_ell == E_ && pr.n_scen == S_ && pr.nx == X_) \
-        return {&launch<Cfg<N_, L_, E_, S_, X_, M_>>, Cfg<N_, L_, E_, S_, X_, M_>::QPM};
-    MPCG_INST(20, 4, 4, 0, 5, 0)    // C1
-    MPCG_INST(20, 8, 8, 0, 5, 0)    // C2 (north star)
-    MPCG_INST(30, 12, 12, 0, 5, 0)  // C4
-    MPCG_INST(20, 0, 0, 24, 6, 0)   // C5 (SH-MPC, slack model)
-    MPCG_INST(30, 0, 0, 12, 6, 1)   // C3 (curvature-aware bicycle + decomp)
-    MPCG_INST(10, 2, 2, 0, 5, 0)    // small test instances
-    MPCG_INST(10, 0, 0, 4, 6, 0)
-    MPCG_INST(10, 0, 0, 4, 6, 1)
-#undef MPCG_INST
+    std::lock_guard<std::mutex> l(registry_mutex());
+    for (const Inst& in : registry())
+        if (in.model == pr.model && in.N == pr.N && in.nl == pr.n_lin && in.ne == pr.n_ell && in.ns == pr.n_scen &&
+            in.nx == pr.nx)
+            return in;
     return {};
+}
+
+using Fn = mpcg_instance_launch;
+
+static int launch(Fn fn, const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream) {
+    const int e = fn(&pr, batch, &io, (void*)stream, g_stamps);
+    if (e != (int)hipSuccess) {
+        g_err = std::string("sqp_kernel launch: ") + hipGetErrorString((hipError_t)e);
+        return -1;
+    }
+    return 0;
 }
 
 static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
@@ -136,6 +134,21 @@ static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
 }
 
 }  // namespace mpcg
+
+extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx,
+                                      mpcg_instance_launch fn, int qp_mem_size) {
+    if (!fn) return -1;
+    std::lock_guard<std::mutex> l(mpcg::registry_mutex());
+    for (const mpcg::Inst& in : mpcg::registry())
+        if (in.model == model && in.N == N && in.nl == n_lin && in.ne == n_ell && in.ns == n_scen && in.nx == nx)
+            return 0;
+    mpcg::Inst in;
+    in.model = model; in.N = N; in.nl = n_lin; in.ne = n_ell; in.ns = n_scen; in.nx = nx;
+    in.fn = fn;
+    in.qpm = qp_mem_size;
+    mpcg::registry().push_back(in);
+    return 0;
+}
 
 // Persistent context (include/mpcg.h): one device allocation for every
 // buffer of `max_batch` solves, one pinned staging block, a private stream.
@@ -287,7 +300,7 @@ int mpcg_solve(const mpcg_problem* pr, int batch, const mpcg_io* io, void* strea
         mpcg::g_err = "missing buffer";
         return -1;
     }
-    return fn(*pr, batch, *io, (hipStream_t)stream);
+    return mpcg::launch(fn, *pr, batch, *io, (hipStream_t)stream);
 }
 
 int mpcg_solve_batch_device(const mpcg_problem* pr, int batch, const double* params, const double* warm,

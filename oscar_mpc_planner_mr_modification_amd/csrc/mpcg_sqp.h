@@ -410,6 +410,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #endif
     const int sol = blockIdx.x;
     if (sol >= batch) return;
+    // the lane exchanges assume one wavefront per workgroup (wave_sync): any other launch
+    // shape reports an invalid exit code instead of racing
+    if (blockDim.x != 64) {
+        if (threadIdx.x == 0) io.exit_code[sol] = -1;
+        return;
+    }
     const int lane = threadIdx.x;
     const int k = lane / PARTS;          // my stage
     const int part = lane - k * PARTS;   // my part

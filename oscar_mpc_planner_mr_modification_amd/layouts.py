@@ -258,6 +258,11 @@ def config_layout(cfg: str) -> Layout:
         return tmpc_layout(N=20, max_obstacles=8, name="C2")
     if cfg == "C4":
         return tmpc_layout(N=30, max_obstacles=12, name="C4")
+    if cfg == "JS":
+        # the reference's shipped jackalsimulator solver: configuration_tmpc_consistency_cost
+        # (generate_jackalsimulator_solver.py:147) with N 30, max_obstacles 4
+        # (mpc_planner_jackalsimulator/config/settings.yaml:3,37); n_paths 4 -> 5 planners (:104)
+        return tmpc_layout(N=30, max_obstacles=4, name="JS")
     if cfg == "C5":
         lay = safe_horizon_layout(N=20, n_constraints=24)
         lay.name = "C5"

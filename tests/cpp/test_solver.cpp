@@ -227,7 +227,10 @@ static void load(Solver& s, const Batch& b, int i) {
 static void dump(std::ofstream& o, const Solver& s, int code) {
     o.write(reinterpret_cast<const char*>(s._output.xtraj), sizeof(s._output.xtraj));
     o.write(reinterpret_cast<const char*>(s._output.utraj), sizeof(s._output.utraj));
-    double extra[3] = {s._info.pobj, (double)code, (double)s._info.sqp_iter};
+    // AcadosInfo as the reference fills it (acados_solver_interface.cpp:151-164, 193-194)
+    double extra[9] = {s._info.pobj, (double)code, (double)s._info.sqp_iter, (double)s._info.qp_status,
+                       s._info.nlp_res, s._info.kkt_norm_inf, s._info.elapsed_time, s._info.solvetime,
+                       s._info.min_time};
     o.write(reinterpret_cast<const char*>(extra), sizeof extra);
 }
 

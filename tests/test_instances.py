@@ -1,0 +1,102 @@
+"""Kernel instances for any generated solver (mpcg_instance.h): the built-in table
+covers C1-C5 and the reference's shipped robot solvers, and a generated solver of
+other dimensions brings its own instance (codegen mpcg_instance.hip) that
+registers with libmpcg.so when its library loads.  CPU: registration and the
+generated source; GPU: parity of a generated instance and of the shipped
+jackalsimulator shape against the oracle."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "oscar_mpc_planner_mr_modification_amd")
+G25 = os.path.join(PKG, "build", "G25", "libmpcg_inst_G25.so")
+
+
+def _g25():
+    from oscar_mpc_planner_mr_modification_amd.layouts import tmpc_layout
+    return tmpc_layout(N=25, max_obstacles=3, name="G25")
+
+
+def test_codegen_writes_the_instance_of_the_generated_dimensions(tmp_path):
+    from oscar_mpc_planner_mr_modification_amd import codegen
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    codegen.generate(config_layout("JS"), str(tmp_path))
+    src = open(tmp_path / "mpcg_instance.hip").read()
+    assert "MPCG_DEFINE_INSTANCE(30, 4, 4, 0, 5, 0)" in src
+    codegen.generate(config_layout("C3"), str(tmp_path))
+    assert "MPCG_DEFINE_INSTANCE(30, 0, 0, 12, 6, 1)" in open(tmp_path / "mpcg_instance.hip").read()
+
+
+def test_shipped_robot_solvers_have_builtin_instances():
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout, tmpc_layout
+    from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
+    lib = C.CDLL(os.path.join(PKG, "libmpcg.so"))
+    # jackalsimulator (N 30, 4 obstacles), jackal / dingo (N 30, 5 obstacles)
+    for lay in (config_layout("JS"), tmpc_layout(N=30, max_obstacles=5)):
+        assert lib.mpcg_supported(C.byref(problem_from_layout(lay))) == 0, lay.name
+
+
+def test_generated_instance_registers_on_load():
+    """In a fresh process: the G25 shape is unknown to libmpcg.so until the generated
+    instance library is loaded (no GPU call: registration is host code)."""
+    code = f"""
+import ctypes as C, sys
+sys.path.insert(0, {ROOT!r})
+from oscar_mpc_planner_mr_modification_amd.layouts import tmpc_layout
+from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
+lib = C.CDLL({os.path.join(PKG, "libmpcg.so")!r}, mode=C.RTLD_GLOBAL)
+pr = problem_from_layout(tmpc_layout(N=25, max_obstacles=3))
+before = lib.mpcg_supported(C.byref(pr))
+C.CDLL({G25!r}, mode=C.RTLD_GLOBAL)
+after = lib.mpcg_supported(C.byref(pr))
+lib.mpcg_qp_mem_size.restype = C.c_int
+print(before, after, lib.mpcg_qp_mem_size(C.byref(pr)))
+"""
+    if not os.path.exists(G25):
+        from oscar_mpc_planner_mr_modification_amd import _build
+        _build.build_instance(_g25(), os.path.dirname(G25))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    before, after, qpm = (int(v) for v in r.stdout.split())
+    assert (before, after) == (-1, 0)
+    assert qpm > 0
+
+
+def _parity(native, oracle_mod, lay, S, G, seed):
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+    b = make_batch(lay, S, G, seed=seed)
+    ref = oracle_mod.Oracle(lay).solve_batch(b.params, b.warm, b.xinit)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    out = native.solve_batch_device(native.problem_from_layout(lay), t(b.params), t(b.warm), t(b.xinit))
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    same = got["exit"] == ref["status"]
+    ok = same & (got["exit"] == 1)
+    dx = np.abs(got["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
+    print(f"{lay.name}: {len(same)} solves, success {ok.mean():.2f}, max|dx| {dx[ok].max():.2e}")
+    assert same.all()
+    assert ok.mean() >= 0.8
+    assert dx[ok].max() <= 1e-4
+
+
+@pytest.mark.gpu
+def test_generated_instance_parity_on_gpu(oracle_mod):
+    from oscar_mpc_planner_mr_modification_amd import native
+    lay = _g25()
+    native.load_instances(G25)
+    assert native.supported(native.problem_from_layout(lay))
+    _parity(native, oracle_mod, lay, 8, 8, 2525)
+
+
+@pytest.mark.gpu
+def test_jackalsimulator_shipped_solver_parity_on_gpu(oracle_mod):
+    """mpc_planner_jackalsimulator as shipped: N 30, 4 obstacles, 4 guided + 1 non-guided planners."""
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    _parity(native, oracle_mod, config_layout("JS"), 16, 5, 3030)
