@@ -148,8 +148,9 @@ typedef struct mpcg_io {
     int *exit_code, *info;
     double *lam_out;
     /* ABI 5: the capsule's QP memory [batch][mpcg_qp_mem_size] in / out (HPIPM's qp_sol,
-     * kept between Solver::solve() calls; NULL qp_in = a fresh or reset capsule, whose
-     * first QP starts cold: ocp_nlp_solver_reset_qp_memory, acados_solver_interface.cpp:189),
+     * kept between Solver::solve() calls: the first QP's initial point with
+     * qp_warm_start 2, and the bound multipliers of the NLP residuals; NULL qp_in = a
+     * fresh or reset capsule: ocp_nlp_solver_reset_qp_memory, acados_solver_interface.cpp:189),
      * and the NLP residuals [batch][MPCG_STATS_STRIDE]; each may be NULL.  A solve whose
      * qp_in block starts with a NaN has no QP memory (mixed batches of fresh and carried
      * solvers) */

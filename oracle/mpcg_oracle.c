@@ -1034,7 +1034,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
 
     /* the capsule's QP memory (HPIPM's qp_sol: step, pi, slacks, multipliers of the last QP) */
     int have_qp = 0;
-    if (qp_in && pr->qp_warm_start == 2 && !isnan(qp_in[0])) {
+    if (qp_in && !isnan(qp_in[0])) {
         for (int k = 0; k <= N; k++) {
             qp_stage *S = &w.st[k];
             const double *q = qp_in + (size_t)k * qstride;

@@ -30,8 +30,14 @@ namespace mpcg {
 
 template <class C>
 int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps) {
-    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync)
-    hipLaunchKernelGGL((sqp_kernel<C>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io, stamps);
+    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
+    // the NLP-residual variant only when the caller asks for them
+    if (io->stats)
+        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
+                           stamps);
+    else
+        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
+                           stamps);
     return (int)hipGetLastError();
 }
 

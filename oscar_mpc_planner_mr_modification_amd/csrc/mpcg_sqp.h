@@ -395,7 +395,11 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
     }
 }
 
-template <class C>
+// STATS: the variant that also evaluates the NLP residuals of every linearisation
+// (mpcg_io.stats; the drop-in's AcadosInfo).  A separate instance, so that the batched
+// path without it keeps its register allocation (the residual pass holds the previous
+// QP's row multipliers across the linearisation: 68 B/lane of scratch on C2 / C5).
+template <class C, bool STATS = false>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
@@ -519,11 +523,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     for (int e = lane; e < N * NX; e += 64)
         (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
     for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
-    // HPIPM warm start (qp_solver_warm_start 2): the QP memory of the capsule, if any, is the
-    // initial point of the first QP; the later QPs start from their predecessor's solution
+    // the capsule's QP memory, if any: the previous QP's solution, whose row multipliers are
+    // also the NLP's (FIXED_STEP) -- read by the NLP residuals -- and, with the HPIPM warm
+    // start (qp_solver_warm_start 2), the initial point of the first QP; the later QPs
+    // start from their predecessor's solution
     const bool qp_warm = pr.qp_warm_start == 2;
     bool have_qp = false;
-    if (qp_warm && io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
+    if (io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
         const double* q = io.qp_in + (size_t)sol * C::QPM;
 #pragma unroll
         for (int sl = 0; sl < C::SLOTS; ++sl) {
@@ -681,7 +687,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
         // =============== feedback: QP by Riccati interior point ===============
         STAMP_BEGIN();
-        if (io.stats) {
+        if (STATS) {
             // NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
             // multipliers the NLP holds: pi_nlp and, per row, the previous QP's multiplier
             // (FIXED_STEP: lam = lam_qp) or, before any QP, the carried h-row ones (box 0)
@@ -1840,7 +1846,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         for (int e = lane; e < (N + 1) * NZ; e += 64) q[C::QPM_ROWS + e] = (&S.dz[0][0])[e];
         for (int e = lane; e < N * NX; e += 64) q[C::QPM_ROWS + (N + 1) * NZ + e] = (&S.piq[0][0])[e];
     }
-    if (io.stats && lane == 0) {
+    if (STATS && lane == 0) {
         double* st = io.stats + (size_t)sol * MPCG_STATS_STRIDE;
         st[0] = nlp_stat;
         st[1] = res_eq;
