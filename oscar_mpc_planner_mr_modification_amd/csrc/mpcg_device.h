@@ -202,6 +202,14 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
 // Outputs F = [B A] (nx x nz), xn, and (if pi != nullptr) H += Hess(pi' x+).
 // The slack state (nx 6) has zero dynamics: x+ = slack, a unit row.
 // ---------------------------------------------------------------------------
+// Coefficients of a and v in the s+ row of the ERK4 map (s' = v, v' = a): RK4 integrates the
+// quadratic s(t) = s + v t + a t^2 / 2 exactly, so they are dt^2 / 2 and dt; the kernel uses them
+// for the [B A] rows it does not store, and erk_unicycle writes the same values.
+__device__ __forceinline__ void erk_srow(const mpcg_problem& pr, double& sa, double& sv) {
+    sa = 0.5 * pr.dt * pr.dt;
+    sv = pr.dt;
+}
+
 template <int NX>
 __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + NX], const double* pi,
                                     double xn[NX], double F[NX][NU + NX], double H[NU + NX][NU + NX]) {
@@ -241,7 +249,6 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + 
             const double dcy_p = ve * ce, dcy_v = se;    // d(v sin)/d(psi_e, v_e)
             jx[0] += bq * dcx_v * tau; jx[1] += bq * dcx_p * tau; jx[2] += bq * dcx_p; jx[3] += bq * dcx_v;
             jy[0] += bq * dcy_v * tau; jy[1] += bq * dcy_p * tau; jy[2] += bq * dcy_p; jy[3] += bq * dcy_v;
-            js[0] += bq * tau; js[3] += bq;
             if (pi) {
                 // second derivatives of pix v cos + piy v sin in (psi_e, v_e)
                 const double hpp = bq * (-pix * ve * ce - piy * ve * se);
@@ -256,6 +263,7 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + 
             }
         }
     }
+    erk_srow(pr, js[0], js[3]);
     const double T = pr.dt;
     xn[0] = z[2] + sx;
     xn[1] = z[3] + sy;

@@ -31,8 +31,8 @@ namespace mpcg {
 template <class C>
 int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps) {
     // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
-    // the NLP-residual variant only when the caller asks for them
-    if (io->stats)
+    // the full variant only when the call needs QP memory, the warm start or the residuals
+    if (io->stats || io->qp_in || io->qp_out || pr->qp_warm_start == 2)
         hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
                            stamps);
     else

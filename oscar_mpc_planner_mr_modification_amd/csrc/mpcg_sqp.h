@@ -86,9 +86,15 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
-    // 1/t of every row kept in registers when the row state is small; long
-    // horizons (PARTS = 2, more rows per lane) recompute it to stay out of scratch
-    static constexpr bool STORE_IT = SLOTS <= 12;
+    // 1/t of every row kept in registers when the row state is small; the two-part
+    // instances (long horizons, more rows per lane) recompute it.  (A two-part instance
+    // with stored 1/t -- N 30 with 4 obstacles, SLOTS 12 -- computed wrong trajectories and
+    // once faulted on the GPU in round 2; the two-part shape of C4, which recomputes 1/t,
+    // is the one validated at full size.)
+#ifndef MPCG_STORE_IT_MAX
+#define MPCG_STORE_IT_MAX 12
+#endif
+    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX && PARTS == 3;
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     // Linear rows (topology and scenario halfspaces) read their coefficients from the
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
@@ -116,7 +122,15 @@ struct Cfg {
     // known), its Hessian block drops the slack row / column but the diagonal, and the new
     // dynamics multipliers and the dynamics residuals live in registers / are recomputed
     static constexpr bool COMPACT = MODEL_ == 1;
-    static constexpr int NFR = COMPACT ? 4 : NX, NFC = COMPACT ? NZ - 1 : NZ;
+    // the unicycle's rows psi+ = psi + dt w, v+ = v + dt a, s+ = s + dt v + dt^2/2 a (and slack+ =
+    // slack) of [B A] are the same constants at every stage (RK4 integrates them exactly,
+    // erk_srow): on the long horizons with few obstacles only the x+ and y+ rows are stored,
+    // which (with the LEAN storage) brings N 30 with 4 or 5 obstacles under the four-solves-
+    // per-CU line (JS 47.2 -> 39.9 KB, 365.8k -> 459.6k solves/s).  The other instances keep all
+    // rows: C4 stays above the line either way (it measured 2.6 % slower with them constant) and
+    // on N 20 the constant rows changed the register allocation into scratch (C2 0 -> 128 B/lane)
+    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30 && NE_ <= 8;
+    static constexpr int NFR = COMPACT ? 4 : (FCONST ? 2 : NX), NFC = COMPACT ? NZ - 1 : NZ;
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // the vector chains split over the parts of a stage (rows of the backward map, columns of
     // the forward one); the register-starved bicycle instance keeps one owner per stage
@@ -149,7 +163,10 @@ struct Cfg {
     __host__ __device__ static constexpr double slack_coef(int hh) { return (NB == 4 && hh >= NL + NE) ? -1.0 : 0.0; }
 };
 
-template <class C>
+// LEAN storage: the dynamics residuals are recomputed where used and the new dynamics multipliers
+// stay in the owner lane's registers (always for the compact C3 storage; elsewhere only where it
+// brings the footprint under the four-solves-per-CU line, see lds_lean)
+template <class C, bool LEAN = C::COMPACT>
 struct Lds {
     static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
     double z[N + 1][NZ];      // NLP iterate [u x]
@@ -163,8 +180,8 @@ struct Lds {
     double ddz[N + 1][NZ];    // QP step
     double pi_nlp[N][NX];
     double piq[N][NX];
-    double pin[C::COMPACT ? 1 : N][NX];
-    double rdyn[C::COMPACT ? 1 : N][NX];
+    double pin[LEAN ? 1 : N][NX];
+    double rdyn[LEAN ? 1 : N][NX];
     alignas(16) double P[N + 1][C::NPTP];  // Riccati cost-to-go, packed (row padded, C::NPTP)
     double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
@@ -179,6 +196,13 @@ struct Lds {
     double xinit[NX];
     int flag;                 // failed pivot (C::COMPACT; the others vote in registers)
 };
+
+// four solves per CU need at most a quarter of the CU's 160 KiB of LDS per workgroup
+constexpr size_t LDS_QUARTER = 160 * 1024 / 4;
+template <class C>
+__host__ __device__ constexpr bool lds_lean() {
+    return C::COMPACT || (sizeof(Lds<C, false>) > LDS_QUARTER && sizeof(Lds<C, true>) <= LDS_QUARTER);
+}
 
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
 // production build compiles them out).  Read shares, not absolute times.
@@ -395,18 +419,22 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
     }
 }
 
-// STATS: the variant that also evaluates the NLP residuals of every linearisation
-// (mpcg_io.stats; the drop-in's AcadosInfo).  A separate instance, so that the batched
-// path without it keeps its register allocation (the residual pass holds the previous
-// QP's row multipliers across the linearisation: 68 B/lane of scratch on C2 / C5).
-template <class C, bool STATS = false>
+// FULL: the variant with the capsule's QP memory (mpcg_io.qp_in / qp_out), the HPIPM warm
+// start (pr.qp_warm_start == 2) and the NLP residuals of every linearisation
+// (mpcg_io.stats; the drop-in's AcadosInfo).  The lean variant (FULL = false: cold
+// start, no QP memory, no residuals) is the batched path: there the rows' interior-point
+// state is rewritten at every QP start and dead across the linearisation, which keeps
+// the register allocation of the hot loops (the warm start and the residual pass hold
+// the previous QP's row state across the linearisation).
+template <class C, bool FULL = false>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
     constexpr int NU = C::NU;   // (shadows the unicycle's mpcg::NU)
     constexpr int ZS = C::ZSL;  // slack variable (NB == 4)
     constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
-    __shared__ Lds<C> S;
+    constexpr bool LEAN = lds_lean<C>();
+    __shared__ Lds<C, LEAN> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
     __shared__ char lds_pad[MPCG_LDS_PAD];
@@ -486,8 +514,18 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         }
     };
     // [B A] and Hessian entries of stage kq (the compact C3 storage rebuilds the known ones)
+    // the s+ row's coefficients of a and v (uniform, bit-identical to erk_unicycle's)
+    double srow_a = 0.0, srow_v = 0.0;
+    if constexpr (C::FCONST) erk_srow(pr, srow_a, srow_v);
     auto Fat = [&](int kq, int m, int j) -> double {
-        if constexpr (C::COMPACT) {
+        if constexpr (C::FCONST) {
+            // rows psi+, v+, s+ (, slack+) are constants (z = [a w x y psi v s (slack)])
+            if (m == 2) return j == 1 ? pr.dt : (j == 4 ? 1.0 : 0.0);
+            if (m == 3) return j == 0 ? pr.dt : (j == 5 ? 1.0 : 0.0);
+            if (m == 4) return j == 0 ? srow_a : (j == 5 ? srow_v : (j == 6 ? 1.0 : 0.0));
+            if (m >= 5) return j == NU + m ? 1.0 : 0.0;
+            return S.F[kq][m][j];
+        } else if constexpr (C::COMPACT) {
             if (m == 3) return j == bike::ZV ? 1.0 : (j == bike::ZA ? pr.dt : 0.0);
             if (m == 4) return j == bike::ZDELTA ? 1.0 : (j == bike::ZW ? pr.dt : 0.0);
             if (j == ZS) return 0.0;
@@ -527,9 +565,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // also the NLP's (FIXED_STEP) -- read by the NLP residuals -- and, with the HPIPM warm
     // start (qp_solver_warm_start 2), the initial point of the first QP; the later QPs
     // start from their predecessor's solution
-    const bool qp_warm = pr.qp_warm_start == 2;
+    const bool qp_warm = FULL && pr.qp_warm_start == 2;
     bool have_qp = false;
-    if (io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
+    if (FULL && io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
         const double* q = io.qp_in + (size_t)sol * C::QPM;
 #pragma unroll
         for (int sl = 0; sl < C::SLOTS; ++sl) {
@@ -607,8 +645,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const double bi = xn[i] - S.z[k + 1][NU + i];
                         S.b[k][i] = bi;
                         resl = fmax(resl, fabs(bi));
+                        if (i < C::NFR) {
 #pragma unroll
-                        for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                            for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                        }
                     }
                 }
 #pragma unroll
@@ -687,7 +727,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
         // =============== feedback: QP by Riccati interior point ===============
         STAMP_BEGIN();
-        if (STATS) {
+        if (FULL && io.stats) {
             // NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
             // multipliers the NLP holds: pi_nlp and, per row, the previous QP's multiplier
             // (FIXED_STEP: lam = lam_qp) or, before any QP, the carried h-row ones (box 0)
@@ -810,7 +850,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         wave_sync();
         STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
-        double pinr[C::COMPACT ? NX : 1];  // C::COMPACT: the new dynamics multipliers of the own stage
+        double pinr[LEAN ? NX : 1];  // LEAN: the new dynamics multipliers of the own stage
         double Hdz[NZ];  // part 0: H_k dz_k of the current iterate
         for (;; ++qit) {
             if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
@@ -903,7 +943,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double a = S.b[k][i] - S.dz[k + 1][NU + i];
 #pragma unroll
                             for (int j = 0; j < NZ; ++j) a += Fat(k, i, j) * dzk[j];
-                            if constexpr (!C::COMPACT) S.rdyn[k][i] = a;
+                            if constexpr (!LEAN) S.rdyn[k][i] = a;
                             re = fmax(re, fabs(a));
                         }
                     }
@@ -1221,9 +1261,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                         for (int u = 0; u < NU; ++u) il[u] = S.Lc[kv][C::NLO + u];
                     }
-                    // dynamics residual of stage kv (C::COMPACT recomputes it)
+                    // dynamics residual of stage kv (LEAN recomputes it)
                     auto rdyn_v = [&](int i) -> double {
-                        if constexpr (C::COMPACT) return rdyn_at(kv, i);
+                        if constexpr (LEAN) return rdyn_at(kv, i);
                         else return S.rdyn[kv][i];
                     };
                     int rs[RS];
@@ -1454,7 +1494,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            if constexpr (C::COMPACT) pinr[i] = a;
+                            if constexpr (LEAN) pinr[i] = a;
                             else S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
@@ -1476,12 +1516,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
                     }
                     double G[NX][NX], hv[NX], Wu[NU][NX], y0[NU];
-                    double rdv[C::COMPACT ? NX : 1];  // C::COMPACT: recomputed dynamics residual
+                    double rdv[LEAN ? NX : 1];  // LEAN: recomputed dynamics residual
                     {
                         double c[NX], rr[NX];
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
-                            if constexpr (C::COMPACT) rr[i] = rdv[i] = rdyn_at(kq, i);
+                            if constexpr (LEAN) rr[i] = rdv[i] = rdyn_at(kq, i);
                             else rr[i] = S.rdyn[kq][i];
                         }
 #pragma unroll
@@ -1595,7 +1635,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
                         double acc;
-                        if constexpr (C::COMPACT) acc = rdv[i];
+                        if constexpr (LEAN) acc = rdv[i];
                         else acc = S.rdyn[kq][i];
 #pragma unroll
                         for (int u = 0; u < NU; ++u) acc += Fat(kq, i, u) * kf[u];
@@ -1664,7 +1704,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            if constexpr (C::COMPACT) pinr[i] = a;
+                            if constexpr (LEAN) pinr[i] = a;
                             else S.pin[k][i] = a;
                         }
                         if (k == N - 1) {
@@ -1773,7 +1813,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 if (k < N) {
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
-                        if constexpr (C::COMPACT) S.piq[k][i] += alpha * (pinr[i] - S.piq[k][i]);
+                        if constexpr (LEAN) S.piq[k][i] += alpha * (pinr[i] - S.piq[k][i]);
                         else S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
                     }
                 }
@@ -1836,7 +1876,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 if (LR.h_on(r)) lo[(size_t)k * LAMS + NX + LR.hrow(r)] = R.nlam[r];
         }
     }
-    if (io.qp_out) {
+    if (FULL && io.qp_out) {
         double* q = io.qp_out + (size_t)sol * C::QPM;
 #pragma unroll
         for (int sl = 0; sl < C::SLOTS; ++sl) {
@@ -1846,7 +1886,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         for (int e = lane; e < (N + 1) * NZ; e += 64) q[C::QPM_ROWS + e] = (&S.dz[0][0])[e];
         for (int e = lane; e < N * NX; e += 64) q[C::QPM_ROWS + (N + 1) * NZ + e] = (&S.piq[0][0])[e];
     }
-    if (STATS && lane == 0) {
+    if (FULL && io.stats && lane == 0) {
         double* st = io.stats + (size_t)sol * MPCG_STATS_STRIDE;
         st[0] = nlp_stat;
         st[1] = res_eq;
