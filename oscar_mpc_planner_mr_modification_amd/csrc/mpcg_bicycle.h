@@ -221,14 +221,16 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
 // five bicycle states, then the CA spline update.  Outputs xn, the rows of
 // [B A] of x+, y+, psi+ and s+ without the slack column (written straight to
 // `F`, LDS in the kernel; the rows of v+ = v + dt a and delta+ = delta + dt w
-// are known) and Hp = Hess(pi' x+) packed (lower triangle over z, sym index).
+// are known) and Hs = Hess(pi' x+) packed without the slack row / column (lower triangle,
+// tri(fc(i), fc(j)); the slack couples to nothing): the stage's LDS Hessian block, so that
+// the 36 entries are not held in registers through the spline update.
 // RK jets over 0 a, 1 w, 2 psi, 3 v, 4 delta; x and y enter the integrated
 // positions additively (x+ = x + dX, y+ = y + dY), so dp = (dX, dY) in the update.
 // Written to keep few jets live at once (the linearisation lane's registers):
 // F rows and the psi Hessian leave before the update is evaluated.
 // ---------------------------------------------------------------------------
-__device__ inline void discrete(const mpcg_problem& pr, const double* __restrict__ p, const double z[NZB],
-                                const double* pi, double xn[NXB], double (*F)[NZB - 1], double Hp[NZB * (NZB + 1) / 2]) {
+__device__ __forceinline__ void discrete(const mpcg_problem& pr, const double* __restrict__ p, const double z[NZB],
+                                const double* pi, double xn[NXB], double (*F)[NZB - 1], double* Hs) {
     const int ns = pr.rk_steps;
     const double h = pr.dt / ns;
     // v' = a and delta' = w are integrated exactly (v_q = v + tau a, delta_q = delta + tau w at
@@ -286,12 +288,13 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
     F[0][fc(ZX)] = 1.0;
     F[1][fc(ZY)] = 1.0;
     const double p2 = pi ? pi[2] : 0.0;
+    constexpr auto hc = [](int i, int j) { return tri(i < ZSL ? i : i - 1, j < ZSL ? j : j - 1); };
 #pragma unroll
-    for (int i = 0; i < NZB * (NZB + 1) / 2; ++i) Hp[i] = 0.0;
+    for (int i = 0; i < (NZB - 1) * NZB / 2; ++i) Hs[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
-        for (int j = 0; j <= i; ++j) Hp[tri(ri[i], ri[j])] = p2 * psi.h[tri(i, j)];
+        for (int j = 0; j <= i; ++j) Hs[hc(ri[i], ri[j])] = p2 * psi.h[tri(i, j)];
 
     // ---- CA spline update (solver_model.py:409-437); local jets 0 x, 1 y, 2 s, 3 dpx, 4 dpy
     PathJets PJ;
@@ -329,17 +332,17 @@ __device__ inline void discrete(const mpcg_problem& pr, const double* __restrict
         const double gyi = ps * (G.h[tri(4, 3)] * dX.g[i] + G.h[tri(4, 4)] * dY.g[i]);
 #pragma unroll
         for (int j = 0; j <= i; ++j)
-            Hp[tri(ri[i], ri[j])] += cX * dX.h[tri(i, j)] + cY * dY.h[tri(i, j)] + gxi * dX.g[j] + gyi * dY.g[j];
+            Hs[hc(ri[i], ri[j])] += cX * dX.h[tri(i, j)] + cY * dY.h[tri(i, j)] + gxi * dX.g[j] + gyi * dY.g[j];
     }
     // (x, y, s) block and its coupling with (a, w, psi, v, delta) through (dpx, dpy)
     constexpr int ui[3] = {ZX, ZY, ZS};
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
 #pragma unroll
-        for (int n = 0; n <= m; ++n) Hp[tri(ui[m], ui[n])] += ps * G.h[tri(m, n)];
+        for (int n = 0; n <= m; ++n) Hs[hc(ui[m], ui[n])] += ps * G.h[tri(m, n)];
         const double c3 = ps * G.h[tri(3, m)], c4 = ps * G.h[tri(4, m)];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) Hp[tri(ui[m], ri[j])] += c3 * dX.g[j] + c4 * dY.g[j];
+        for (int j = 0; j < 5; ++j) Hs[hc(ui[m], ri[j])] += c3 * dX.g[j] + c4 * dY.g[j];
     }
 }
 

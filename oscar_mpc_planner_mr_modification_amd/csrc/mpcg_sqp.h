@@ -617,17 +617,18 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
                 if constexpr (C::MODEL == 1) {
-                    // the bicycle: the discrete map first (F straight to LDS, its Hessian packed),
-                    // then the cost, so that the map's jets and the 9x9 cost block are not live together
-                    double Hp[C::NTRI];
-                    bike::discrete(pr, pk, zk, pi, xn, S.F[k], Hp);
+                    // the bicycle: the discrete map first (F and its Hessian straight to the stage's
+                    // LDS blocks, H[k] rewritten below), then the cost, so that the map's jets and the
+                    // 9x9 cost block are not live together
+                    bike::discrete(pr, pk, zk, pi, xn, S.F[k], S.H[k]);
                     STAMP_LAP(12);
                     bike::stage_cost(pr, pk, k, zk, g, H, true);
                     STAMP_LAP(11);
 #pragma unroll
                     for (int i = 0; i < NZ; ++i)
 #pragma unroll
-                        for (int j = 0; j < NZ; ++j) H[i][j] += Hp[sym(i, j)];
+                        for (int j = 0; j < NZ; ++j)
+                            if (i != ZS && j != ZS) H[i][j] += S.H[k][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
                         const double bi = xn[i] - S.z[k + 1][NU + i];
