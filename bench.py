@@ -79,7 +79,10 @@ def load_counters(path, config, batch):
         return None, None, f"PMC summary {tj.get('tag')} is for {tj.get('config')} batch {tj.get('batch')}"
     if tj.get("source_sha256") != source_hash():
         return None, None, f"PMC summary {tj.get('tag')} was taken on other kernel sources (stale)"
-    return tj.get("hbm_bytes_per_launch"), tj.get("fp64_issued_flop_per_launch"), f"profiles/{tj.get('tag')}"
+    f64 = tj.get("fp64_issued_flop_per_launch")
+    if f64:
+        f64 = {"flop": f64, "lane_util": tj.get("valu_lane_util")}
+    return tj.get("hbm_bytes_per_launch"), f64, f"profiles/{tj.get('tag')}"
 
 
 # ----------------------------------------------------------------- workloads
@@ -421,10 +424,16 @@ def main():
                 "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps, "counters": counters}
     if f64:
         # the path is fp64-VALU / latency bound: issued fp64 FLOP/s of the solve kernel
-        # (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) against the vector peak
-        roofline["fp64_valu_issued"] = {"achieved_tflops": round(f64 / (kern_ms * 1e-3) / 1e12, 3),
-                                        "peak_tflops": FP64_VALU_PEAK_TFLOPS,
-                                        "frac": f64 / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS}
+        # (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) against the vector peak, and
+        # the useful share: issued x the VALU lane utilisation (rocprofv3 VALUUtilization, the
+        # kernel's average active-lane fraction, applied to its fp64 instructions)
+        tf = f64["flop"] / (kern_ms * 1e-3) / 1e12
+        roofline["fp64_valu_issued"] = {"achieved_tflops": round(tf, 3), "peak_tflops": FP64_VALU_PEAK_TFLOPS,
+                                        "frac": tf / FP64_VALU_PEAK_TFLOPS}
+        if f64.get("lane_util"):
+            lu = f64["lane_util"]
+            roofline["fp64_valu_useful"] = {"achieved_tflops": round(tf * lu, 3), "lane_util": round(lu, 4),
+                                            "frac": tf * lu / FP64_VALU_PEAK_TFLOPS}
     if "prepare" in phase_ms and hasattr(wl, "producer_roofline"):
         roofline["producer"] = wl.producer_roofline(phase_ms["prepare"])
     ok = exit_h == 1

@@ -181,7 +181,7 @@ __device__ inline double stage_cost(const mpcg_problem& pr, const double* __rest
     // projection_ratio = 1 / (1 - ((x - px) ddx + (y - py) ddy))  (curvature_aware_contouring.py:83-84)
     const J5 proj = jinv((-1.0) * (ex * jlift(PJ.Z[0], 4) + ey * jlift(PJ.Z[1], 4)) + 1.0);
     double sp, cp;
-    sincos(z[ZPSI], &sp, &cp);
+    fsincos(z[ZPSI], &sp, &cp);
     // s_dot = v (cos psi tx + sin psi ty) projection_ratio  (:85)
     const J5 sdot = (v * (jcos(psi, cp, sp) * tx + jsin(psi, cp, sp) * ty)) * proj;
     const J5 cerr2 = jsq(ex) + jsq(ey);  // (:88)
@@ -250,15 +250,15 @@ __device__ __forceinline__ void discrete(const mpcg_problem& pr, const double* _
             J5 dq = jvar(4, z[ZDELTA] + tau * z[ZW]);
             dq.g[1] = tau;
             // beta = atan(ratio tan delta)
-            const double td = tan(dq.v);
+            const double td = ftan(dq.v);
             const double rt = RATIO * td, ib = frcp(1.0 + rt * rt);
             // d beta / d delta and d2 beta / d delta2 through rt = ratio tan(delta)
             const double rt1 = RATIO * (1.0 + td * td), rt2 = RATIO * 2.0 * td * (1.0 + td * td);
             const J5 beta = jfn(dq, atan(rt), ib * rt1, ib * rt2 - 2.0 * rt * ib * ib * rt1 * rt1);
             const J5 ang = pq + beta;
             double sa, ca, sb, cb;
-            sincos(ang.v, &sa, &ca);
-            sincos(beta.v, &sb, &cb);
+            fsincos(ang.v, &sa, &ca);
+            fsincos(beta.v, &sb, &cb);
             dX = dX + wq * (vq * jcos(ang, ca, sa));
             dY = dY + wq * (vq * jsin(ang, ca, sa));
             kp = ((1.0 / LR) * vq) * jsin(beta, cb, sb);

@@ -47,6 +47,46 @@ __device__ __forceinline__ double frsq(double x) {
 __device__ __forceinline__ double fsqrt_pos(double x) { return x * frsq(x); }
 
 // ---------------------------------------------------------------------------
+// sin and cos of one argument: quadrant n = rint(2x / pi), r = x - n pi/2 by two
+// fused steps (pi/2 as a double pair), then the fdlibm kernel polynomials on
+// [-pi/4, pi/4].  Within ~1 ulp of the correctly rounded values for
+// |x| < 2^20 pi/2 (the angles of this path are headings and steering angles of
+// order one); beyond that the reduction error grows with n.  Unlike the ROCm
+// device library's sincos it has no large-argument (Payne-Hanek) branch, whose
+// registers the linearisation lane otherwise reserves through its jets (the
+// bicycle instance spilled on it).  __host__ too: tests/test_device_math checks
+// it against the C library on the host.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ void fsincos(double x, double* s, double* c) {
+    const double n = rint(x * 0x1.45f306dc9c883p-1);     // 2 / pi
+    double r = fma(-n, 0x1.921fb54442d18p+0, x);           // pi/2, leading double
+    r = fma(-n, 0x1.1a62633145c07p-54, r);                 // pi/2 - leading double
+    r = n == 0.0 ? x : r;
+    const double z = r * r;
+    // __kernel_sin: r + r^3 (S1 + z (S2 + ... S6))
+    const double ps = 0x1.111111110f8a6p-7 + z * (-0x1.a01a019c161d5p-13 + z * (0x1.71de357b1fe7dp-19 +
+                      z * (-0x1.ae5e68a2b9cebp-26 + z * 0x1.5d93a5acfd57cp-33)));
+    double sr = r + (r * z) * (-0x1.5555555555549p-3 + z * ps);
+    sr = fabs(r) < 0x1p-27 ? r : sr;                       // sin r = r there (and sin(-0) = -0)
+    // __kernel_cos: w + (((1 - w) - z/2) + z^2 (C1 + z (C2 + ... C6))), w = 1 - z/2
+    const double pc = 0x1.555555555554cp-5 + z * (-0x1.6c16c16c15177p-10 + z * (0x1.a01a019cb159p-16 +
+                      z * (-0x1.27e4f809c52adp-22 + z * (0x1.1ee9ebdb4b1c4p-29 + z * -0x1.8fae9be8838d4p-37))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + (z * z) * pc);
+    const long q = (long)n & 3;
+    const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// tan through fsincos (within ~3 ulp; cos(x) != 0 for the steering angles it is used on)
+__device__ __forceinline__ double ftan(double x) {
+    double s, c;
+    fsincos(x, &s, &c);
+    return s * frcp(c);
+}
+
+// ---------------------------------------------------------------------------
 // glued spline of spline.py:39-58: for both axes the glued position G and the
 // glued segment-derivative D, each with first and second s-derivatives.
 // ---------------------------------------------------------------------------

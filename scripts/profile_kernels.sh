@@ -21,4 +21,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES \
   -d $o/prof_${tag}_f64 -o run --output-format csv \
   -- python3 bench.py --no-cpu --steps 3 --warmup 1 $extra > $o/prof_${tag}_f64.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES \
+  -d $o/prof_${tag}_lanes -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 $extra > $o/prof_${tag}_lanes.log 2>&1
 echo profile-done

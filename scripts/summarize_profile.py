@@ -52,7 +52,7 @@ def main():
     shutil.copy(os.path.join(src, f"prof_{tag}_trace", "run_kernel_stats.csv"),
                 os.path.join(out, f"{tag}_kernel_stats.csv"))
     pmc, meta = {}, {}
-    for p in ("fetch", "write", "sq", "f64"):
+    for p in ("fetch", "write", "sq", "f64", "lanes"):
         f = os.path.join(src, f"prof_{tag}_{p}", "run_counter_collection.csv")
         if os.path.exists(f):
             c, m = counters(f)
@@ -77,6 +77,11 @@ def main():
             fl = 64 * (d.get("SQ_INSTS_VALU_ADD_F64", 0) + d.get("SQ_INSTS_VALU_MUL_F64", 0) +
                        2 * d["SQ_INSTS_VALU_FMA_F64"] + d.get("SQ_INSTS_VALU_TRANS_F64", 0))
             e["fp64_issued_flop_per_launch"] = fl
+        if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
+            # rocprofv3's VALUUtilization: active lanes per issued VALU cycle
+            e["valu_lane_util"] = d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"])
+        if "SQ_LDS_BANK_CONFLICT" in d and d.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_bank_conflict_frac"] = d["SQ_LDS_BANK_CONFLICT"] / d["SQ_LDS_IDX_ACTIVE"]
         res["kernels"][k] = e
     pk = res["kernels"].get("prepare_kernel")
     if pk and "hbm_write_bytes" in pk:
@@ -103,7 +108,8 @@ def main():
         tr = {"tag": tag, "config": args.config, "batch": args.batch, "source_sha256": source_hash(),
               "hbm_bytes_per_launch": sq["hbm_bytes_per_launch"],
               "hbm_read_bytes": sq["hbm_read_bytes"], "hbm_write_bytes": sq["hbm_write_bytes"],
-              "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch")}
+              "fp64_issued_flop_per_launch": sq.get("fp64_issued_flop_per_launch"),
+              "valu_lane_util": sq.get("valu_lane_util")}
         json.dump(tr, open(os.path.join(out, f"traffic_{args.config}.json"), "w"), indent=1)
         if args.config == "C2":
             json.dump(tr, open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
