@@ -105,7 +105,7 @@ __device__ __forceinline__ J5 jcos(const J5& a, double c, double s) { return jfn
 __device__ __forceinline__ J5 jsin(const J5& a, double c, double s) { return jfn(a, s, c, -s); }
 __device__ __forceinline__ J5 jatan2(const J5& y, const J5& x) {
     const double r2 = x.v * x.v + y.v * y.v, ir2 = frcp(r2), ir4 = ir2 * ir2;
-    return jfn2(y, x, atan2(y.v, x.v), x.v * ir2, -y.v * ir2, -2.0 * x.v * y.v * ir4, (y.v * y.v - x.v * x.v) * ir4,
+    return jfn2(y, x, fatan2(y.v, x.v, FRcp{}), x.v * ir2, -y.v * ir2, -2.0 * x.v * y.v * ir4, (y.v * y.v - x.v * x.v) * ir4,
                 2.0 * x.v * y.v * ir4);
 }
 
@@ -127,7 +127,7 @@ __device__ inline void path_jets(const mpcg_problem& pr, const double* __restric
         S1 P = {q0, q1, q2}, D = {q1, q2, q3}, Z = {q2, q3, 0.0};
         for (int k = M - 1; k >= 1; --k) {
             const double e = exp((s - base[9 * k + 8] + 0.02) / 0.1);
-            const double l0 = frcp(1.0 + e);
+            const double l0 = e < 0x1p1000 ? frcp(1.0 + e) : 0.0;  // 1 / (1 + inf) = 0, as the oracle
             const double l1 = -10.0 * l0 * (1.0 - l0);
             const double l2 = 100.0 * l0 * (1.0 - l0) * (1.0 - 2.0 * l0);
             const double m0 = 1.0 - l0;
@@ -254,7 +254,7 @@ __device__ __forceinline__ void discrete(const mpcg_problem& pr, const double* _
             const double rt = RATIO * td, ib = frcp(1.0 + rt * rt);
             // d beta / d delta and d2 beta / d delta2 through rt = ratio tan(delta)
             const double rt1 = RATIO * (1.0 + td * td), rt2 = RATIO * 2.0 * td * (1.0 + td * td);
-            const J5 beta = jfn(dq, atan(rt), ib * rt1, ib * rt2 - 2.0 * rt * ib * ib * rt1 * rt1);
+            const J5 beta = jfn(dq, fatan(rt, FRcp{}), ib * rt1, ib * rt2 - 2.0 * rt * ib * ib * rt1 * rt1);
             const J5 ang = pq + beta;
             double sa, ca, sb, cb;
             fsincos(ang.v, &sa, &ca);

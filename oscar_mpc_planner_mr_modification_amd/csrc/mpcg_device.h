@@ -79,6 +79,48 @@ __host__ __device__ __forceinline__ void fsincos(double x, double* s, double* c)
     *c = ((q + 1) & 2) ? -cc : cc;
 }
 
+// atan and atan2 after fdlibm's s_atan / e_atan2: |x| reduced to one of the intervals
+// around 0, 1/2, 1, 3/2, infinity (one quotient, through the reciprocal), the odd
+// polynomial, the interval's atan as a double pair; quadrants and special values by
+// selects, no branches.  Within ~2 ulp of the C library (tests/test_device_math).
+template <class RCP>
+__host__ __device__ __forceinline__ double fatan_abs(double ax, RCP rcp) {
+    // ax = |x| (may be +inf)
+    const int id = ax < 0.4375 ? -1 : (ax < 0.6875 ? 0 : (ax < 1.1875 ? 1 : (ax < 2.4375 ? 2 : 3)));
+    const double num = id == 0 ? 2.0 * ax - 1.0 : (id == 1 ? ax - 1.0 : (id == 2 ? ax - 1.5 : -1.0));
+    const double den = id == 0 ? 2.0 + ax : (id == 1 ? ax + 1.0 : (id == 2 ? 1.0 + 1.5 * ax : ax));
+    double x = id < 0 ? ax : num * rcp(den);
+    x = (id == 3 && !(ax < 0x1p66)) ? -0.0 : x;  // atan(huge or inf) = pi/2
+    const double z = x * x, w = z * z;
+    const double s1 = z * (0.333333333333329318027 + w * (0.142857142725034663711 + w * (0.0909088713343650656196 +
+                      w * (0.0666107313738753120669 + w * (0.0497687799461593236017 + w * 0.0162858201153657823623)))));
+    const double s2 = w * (-0.199999999998764832476 + w * (-0.111111104054623557880 + w * (-0.0769187620504482999495 +
+                      w * (-0.0583357013379057348645 + w * -0.0365315727442169155270))));
+    const double hi = id == 0 ? 4.63647609000806093515e-01 : (id == 1 ? 7.85398163397448278999e-01 :
+                      (id == 2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00));
+    const double lo = id == 0 ? 2.26987774529616870924e-17 : (id == 1 ? 3.06161699786838301793e-17 :
+                      (id == 2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17));
+    return id < 0 ? x - x * (s1 + s2) : hi - ((x * (s1 + s2) - lo) - x);
+}
+// the reciprocal of the quotient: frcp on the device (FRcp), the division on the host (tests)
+struct FRcp {
+    __device__ double operator()(double d) const { return frcp(d); }
+};
+template <class RCP>
+__host__ __device__ __forceinline__ double fatan(double x, RCP rcp) {
+    const double a = fatan_abs(fabs(x), rcp);
+    return x < 0.0 ? -a : (x == 0.0 ? x : a);
+}
+// atan2(y, x) for finite arguments, not both zero
+template <class RCP>
+__host__ __device__ __forceinline__ double fatan2(double y, double x, RCP rcp) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double z = fatan_abs(ax == 0.0 ? INFINITY : ay * rcp(ax), rcp);  // atan |y / x|
+    constexpr double PI = 3.1415926535897931160e+00, PI_LO = 1.2246467991473531772e-16;
+    const double r = (__builtin_signbit(x) && ax != 0.0) ? PI - (z - PI_LO) : z;
+    return __builtin_signbit(y) ? -r : r;
+}
+
 // tan through fsincos (within ~3 ulp; cos(x) != 0 for the steering angles it is used on)
 __device__ __forceinline__ double ftan(double x) {
     double s, c;
@@ -120,7 +162,7 @@ __device__ inline void spline_jets(const mpcg_problem& pr, const double* __restr
         // lambda_k uses the start of segment k (spline.py:37)
         const double sk = base[9 * k + 8];
         const double e = exp((s - sk + 0.02) / 0.1);
-        const double l0 = frcp(1.0 + e);
+        const double l0 = e < 0x1p1000 ? frcp(1.0 + e) : 0.0;  // 1 / (1 + inf) = 0, as the oracle
         const double l1 = -10.0 * l0 * (1.0 - l0);
         const double l2 = 100.0 * l0 * (1.0 - l0) * (1.0 - 2.0 * l0);
         const double* seg = base + 9 * (k - 1);

@@ -34,6 +34,26 @@ int main() {
         }
         printf("range %g sin_ulp %lld cos_ulp %lld\n", R, (long long)ms, (long long)mc);
     }
+    // atan / atan2 with the host division as the reciprocal
+    struct Div {
+        double operator()(double d) const { return 1.0 / d; }
+    };
+    const double aranges[] = {1e-9, 0.3, 1.0, 3.0, 100.0, 1e20};
+    for (double R : aranges) {
+        std::uniform_real_distribution<double> u(-R, R);
+        int64_t ma = 0, m2 = 0;
+        for (int i = 0; i < 400000; ++i) {
+            const double x = u(g), y = u(g);
+            const int64_t a = ulps(mpcg::fatan(x, Div{}), std::atan(x));
+            const int64_t b = ulps(mpcg::fatan2(y, x, Div{}), std::atan2(y, x));
+            ma = a > ma ? a : ma;
+            m2 = b > m2 ? b : m2;
+        }
+        printf("arange %g atan_ulp %lld atan2_ulp %lld\n", R, (long long)ma, (long long)m2);
+    }
+    printf("aspecial %.17g %.17g %.17g %.17g %.17g %d\n", mpcg::fatan2(0.0, -1.0, Div{}), mpcg::fatan2(1.0, 0.0, Div{}),
+           mpcg::fatan2(-1.0, -0.0, Div{}), mpcg::fatan(1e300, Div{}), mpcg::fatan(INFINITY, Div{}),
+           std::signbit(mpcg::fatan(-0.0, Div{})) ? 1 : 0);
     double s, c;
     mpcg::fsincos(-0.0, &s, &c);
     printf("negzero %d %g\n", std::signbit(s) ? 1 : 0, c);

@@ -1,10 +1,12 @@
 """Device math helpers (csrc/mpcg_device.h) checked on the host against the C library.
 
-fsincos replaces the ROCm device library's sincos in the bicycle instance (no
-large-argument branch whose registers the linearisation otherwise holds): it must stay
-within 1 ulp of the C library's sin / cos over the argument ranges the path sees, and
-keep sin(-0) = -0.
+fsincos, fatan and fatan2 replace the ROCm device library's functions in the bicycle
+instance (no large-argument / special-value branches whose registers the linearisation
+otherwise holds): sin / cos within 1 ulp of the C library over the argument ranges the
+path sees (sin(-0) = -0), atan / atan2 within 2 ulp with the IEEE quotient (the device
+uses frcp, itself within 1 ulp), and the atan2 quadrants and limits exact.
 """
+import math
 import os
 import shutil
 import subprocess
@@ -26,5 +28,12 @@ def test_fsincos_within_one_ulp(tmp_path):
     assert len(rows) == 6
     for r in rows:
         assert int(r[3]) <= 1 and int(r[5]) <= 1, r
+    arows = [ln.split() for ln in out if ln.startswith("arange")]
+    assert len(arows) == 6
+    for r in arows:
+        assert int(r[3]) <= 2 and int(r[5]) <= 2, r
+    sp = [float(v) for v in next(ln for ln in out if ln.startswith("aspecial")).split()[1:]]
+    assert sp[0] == math.pi and sp[1] == math.pi / 2 and sp[2] == -math.pi / 2
+    assert sp[3] == math.pi / 2 and sp[4] == math.pi / 2 and sp[5] == 1.0
     neg = next(ln for ln in out if ln.startswith("negzero")).split()
     assert neg[1] == "1" and float(neg[2]) == 1.0
