@@ -24,6 +24,10 @@ typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpc
  * launcher). */
 int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
                            int qp_mem_size);
+/* libmpcg.so's device workspace of `stream` (instances whose stage blocks do not fit the
+ * LDS budget keep them there): at least `bytes`, valid for work enqueued on that stream;
+ * NULL on allocation failure. */
+void* mpcg_stream_workspace(void* stream, size_t bytes);
 }
 
 namespace mpcg {
@@ -32,12 +36,17 @@ template <class C>
 int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps) {
     // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
     // the full variant only when the call needs QP memory, the warm start or the residuals
+    double* gws = nullptr;
+    if constexpr (gfh_doubles<C>() > 0) {
+        gws = (double*)mpcg_stream_workspace(stream, (size_t)batch * gfh_doubles<C>() * sizeof(double));
+        if (!gws) return (int)hipErrorOutOfMemory;
+    }
     if (io->stats || io->qp_in || io->qp_out || pr->qp_warm_start == 2)
         hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
-                           stamps);
+                           stamps, gws);
     else
         hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
-                           stamps);
+                           stamps, gws);
     return (int)hipGetLastError();
 }
 

@@ -150,6 +150,45 @@ extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, in
     return 0;
 }
 
+// Device workspaces per (device, stream) for the instances that keep their stage blocks in
+// global memory (mpcg_instance.h): kernels enqueued on one stream run in order, so one
+// buffer per stream serves them all; a larger request waits for the stream's work before
+// the buffer is replaced.  Kept for the life of the process.
+extern "C" void* mpcg_stream_workspace(void* stream, size_t bytes) {
+    struct Ws {
+        int dev;
+        void* stream;
+        void* ptr;
+        size_t size;
+    };
+    static std::mutex m;
+    static std::vector<Ws> pool;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> l(m);
+    Ws* w = nullptr;
+    for (Ws& e : pool)
+        if (e.dev == dev && e.stream == stream) w = &e;
+    if (!w) {
+        pool.push_back(Ws{dev, stream, nullptr, 0});
+        w = &pool.back();
+    }
+    if (w->size < bytes) {
+        if (w->ptr) {
+            if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return nullptr;
+            (void)hipFree(w->ptr);
+            w->ptr = nullptr;
+            w->size = 0;
+        }
+        if (hipMalloc(&w->ptr, bytes) != hipSuccess) {
+            w->ptr = nullptr;
+            return nullptr;
+        }
+        w->size = bytes;
+    }
+    return w->ptr;
+}
+
 // Persistent context (include/mpcg.h): one device allocation for every
 // buffer of `max_batch` solves, one pinned staging block, a private stream.
 struct mpcg_context {

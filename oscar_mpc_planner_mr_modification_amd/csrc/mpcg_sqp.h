@@ -166,13 +166,19 @@ struct Cfg {
 // LEAN storage: the dynamics residuals are recomputed where used and the new dynamics multipliers
 // stay in the owner lane's registers (always for the compact C3 storage; elsewhere only where it
 // brings the footprint under the four-solves-per-CU line, see lds_lean)
-template <class C, bool LEAN = C::COMPACT>
+//
+// GFH: the stage blocks H and [B A] live in a per-solve global workspace (L2-resident: the
+// solves resident on one XCD hold 128 x ~16 KB) instead of LDS -- for the instances above
+// the four-solves-per-CU line even with the LEAN storage (C3, C4): at one wave per SIMD a
+// CU with three solves leaves a SIMD idle.  They are written once per linearisation and
+// read by the Riccati step (prefetched a stage ahead) and the vector passes.
+template <class C, bool LEAN = C::COMPACT, bool GFH = false>
 struct Lds {
     static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
     double z[N + 1][NZ];      // NLP iterate [u x]
-    double H[N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
+    double H[GFH ? 1 : N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
     double g[N + 1][NZ];
-    double F[N][C::NFR][C::NFC];  // [B A] (C::COMPACT: rows x+ y+ psi+ s+, no slack column)
+    double F[GFH ? 1 : N][C::NFR][C::NFC];  // [B A] (C::COMPACT: rows x+ y+ psi+ s+, no slack column)
     double b[N][NX];          // shooting defects
     double dH[N + 1][C::NDH]; // barrier terms: diag(nz) + h-row block (column-major packed), last = 0
     double q[N + 1][NZ];      // Newton gradient
@@ -202,6 +208,19 @@ constexpr size_t LDS_QUARTER = 160 * 1024 / 4;
 template <class C>
 __host__ __device__ constexpr bool lds_lean() {
     return C::COMPACT || (sizeof(Lds<C, false>) > LDS_QUARTER && sizeof(Lds<C, true>) <= LDS_QUARTER);
+}
+template <class C>
+__host__ __device__ constexpr bool lds_gfh() {
+#ifdef MPCG_NO_GFH
+    return false;
+#else
+    return sizeof(Lds<C, lds_lean<C>(), false>) > LDS_QUARTER && sizeof(Lds<C, lds_lean<C>(), true>) <= LDS_QUARTER;
+#endif
+}
+// doubles of one solve's global workspace (GFH: [B A] blocks, then the Hessian blocks)
+template <class C>
+__host__ __device__ constexpr size_t gfh_doubles() {
+    return lds_gfh<C>() ? (size_t)C::N * C::NFR * C::NFC + (size_t)(C::N + 1) * C::NHP : 0;
 }
 
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
@@ -428,13 +447,15 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
 // the previous QP's row state across the linearisation).
 template <class C, bool FULL = false>
 __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
-                                                    unsigned long long* __restrict__ stamps) {
+                                                    unsigned long long* __restrict__ stamps,
+                                                    double* __restrict__ gws) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
     constexpr int NU = C::NU;   // (shadows the unicycle's mpcg::NU)
     constexpr int ZS = C::ZSL;  // slack variable (NB == 4)
     constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
     constexpr bool LEAN = lds_lean<C>();
-    __shared__ Lds<C, LEAN> S;
+    constexpr bool GFH = lds_gfh<C>();
+    __shared__ Lds<C, LEAN, GFH> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
     __shared__ char lds_pad[MPCG_LDS_PAD];
@@ -459,6 +480,17 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     const double* pbase = io.params + (size_t)sol * N * npar;
     const double* pk = pbase + (size_t)kc * npar;
     (void)stamps;
+    // the stage blocks [B A] (Fb) and H (Hb): LDS, or this solve's global workspace (GFH)
+    double* const gF = GFH ? gws + (size_t)sol * gfh_doubles<C>() : nullptr;
+    double* const gH = GFH ? gF + (size_t)N * C::NFR * C::NFC : nullptr;
+    auto Fb = [&](int kq) -> double (*)[C::NFC] {
+        if constexpr (GFH) return (double (*)[C::NFC])(gF + (size_t)kq * C::NFR * C::NFC);
+        else return S.F[kq];
+    };
+    auto Hb = [&](int kq) -> double* {
+        if constexpr (GFH) return gH + (size_t)kq * C::NHP;
+        else return S.H[kq];
+    };
     STAMP_DECL
 
     // NLP multipliers carried over from the previous solve of this planner
@@ -524,22 +556,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (m == 3) return j == 0 ? pr.dt : (j == 5 ? 1.0 : 0.0);
             if (m == 4) return j == 0 ? srow_a : (j == 5 ? srow_v : (j == 6 ? 1.0 : 0.0));
             if (m >= 5) return j == NU + m ? 1.0 : 0.0;
-            return S.F[kq][m][j];
+            return Fb(kq)[m][j];
         } else if constexpr (C::COMPACT) {
             if (m == 3) return j == bike::ZV ? 1.0 : (j == bike::ZA ? pr.dt : 0.0);
             if (m == 4) return j == bike::ZDELTA ? 1.0 : (j == bike::ZW ? pr.dt : 0.0);
             if (j == ZS) return 0.0;
-            return S.F[kq][m < 3 ? m : 3][j < ZS ? j : j - 1];
+            return Fb(kq)[m < 3 ? m : 3][j < ZS ? j : j - 1];
         } else {
-            return S.F[kq][m][j];
+            return Fb(kq)[m][j];
         }
     };
     auto Hat = [&](int kq, int i, int j) -> double {
         if constexpr (C::COMPACT) {
-            if (i == ZS || j == ZS) return (i == j) ? S.H[kq][C::NHP - 1] : 0.0;
-            return S.H[kq][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
+            if (i == ZS || j == ZS) return (i == j) ? Hb(kq)[C::NHP - 1] : 0.0;
+            return Hb(kq)[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
         } else {
-            return S.H[kq][sym(i, j)];
+            return Hb(kq)[sym(i, j)];
         }
     };
     // dynamics residual b + F dz - dz+ of stage kq at the current QP iterate (same operation order
@@ -620,7 +652,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // the bicycle: the discrete map first (F and its Hessian straight to the stage's
                     // LDS blocks, H[k] rewritten below), then the cost, so that the map's jets and the
                     // 9x9 cost block are not live together
-                    bike::discrete(pr, pk, zk, pi, xn, S.F[k], S.H[k]);
+                    double* const Hd = Hb(k);
+                    bike::discrete(pr, pk, zk, pi, xn, Fb(k), Hd);
                     STAMP_LAP(12);
                     bike::stage_cost(pr, pk, k, zk, g, H, true);
                     STAMP_LAP(11);
@@ -628,7 +661,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     for (int i = 0; i < NZ; ++i)
 #pragma unroll
                         for (int j = 0; j < NZ; ++j)
-                            if (i != ZS && j != ZS) H[i][j] += S.H[k][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
+                            if (i != ZS && j != ZS) H[i][j] += Hd[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
                         const double bi = xn[i] - S.z[k + 1][NU + i];
@@ -648,7 +681,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         resl = fmax(resl, fabs(bi));
                         if (i < C::NFR) {
 #pragma unroll
-                            for (int j = 0; j < NZ; ++j) S.F[k][i][j] = F[i][j];
+                            for (int j = 0; j < NZ; ++j) Fb(k)[i][j] = F[i][j];
                         }
                     }
                 }
@@ -701,28 +734,30 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     for (int i = 0; i < NZ; ++i)
 #pragma unroll
                         for (int j = 0; j <= i; ++j)
-                            if (i != ZS && j != ZS) S.H[k][sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)] = H[i][j];
-                    S.H[k][C::NHP - 1] = H[ZS][ZS];
+                            if (i != ZS && j != ZS) Hb(k)[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)] = H[i][j];
+                    Hb(k)[C::NHP - 1] = H[ZS][ZS];
                 } else {
 #pragma unroll
                     for (int i = 0; i < NZ; ++i)
 #pragma unroll
-                        for (int j = 0; j <= i; ++j) S.H[k][sym(i, j)] = H[i][j];
+                        for (int j = 0; j <= i; ++j) Hb(k)[sym(i, j)] = H[i][j];
                 }
             } else if (stage_lane && k == N) {
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) S.g[N][i] = 0.0;
 #pragma unroll
-                for (int e = 0; e < C::NHP; ++e) S.H[N][e] = 0.0;
+                for (int e = 0; e < C::NHP; ++e) Hb(N)[e] = 0.0;
 #pragma unroll
                 for (int i = NU; i < NZ; ++i) {
-                    if constexpr (C::COMPACT) S.H[N][sym(i - 1, i - 1)] = pr.reg_eps;
-                    else S.H[N][sym(i, i)] = pr.reg_eps;
+                    if constexpr (C::COMPACT) Hb(N)[sym(i - 1, i - 1)] = pr.reg_eps;
+                    else Hb(N)[sym(i, i)] = pr.reg_eps;
                 }
             }
             res_eq = wave_max(resl);
             if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
         }
+        // GFH: the stage lanes' global stores of the blocks complete before any lane reads them
+        if constexpr (GFH) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         wave_sync();
         STAMP_END(0);
 
@@ -1085,7 +1120,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // but the diagonal)
                     auto Hel = [&](int kq) -> double {
                         if constexpr (C::COMPACT) return Hat(kq, ei, ej);
-                        else return S.H[kq][le];
+                        else return Hb(kq)[le];
                     };
                     hv = Hel(N - 1) + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
 #pragma unroll
