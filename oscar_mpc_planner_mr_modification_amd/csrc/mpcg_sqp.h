@@ -141,6 +141,20 @@ struct Cfg {
 #define MPCG_C3_FACFLAT 0
 #endif
     static constexpr bool CHAIN_SPLIT = !COMPACT || MPCG_C3_SPLIT;
+    // the split chains as two-stage composed maps (half the sequential steps; see the
+    // vector passes in sqp_kernel).  Measured against the one-step chains: JS 43.45 ->
+    // 42.20 ms; C2 12.74 -> 13.09, C4 53.34 -> 53.78, C5 19.49 -> 20.07 (the compositions
+    // and the extra live state cost more than the halved chain there), so only the long
+    // horizons with the constant-row storage use them.  MPCG_PAIR_ALL / MPCG_NO_PAIR: A/B.
+#if defined(MPCG_NO_PAIR)
+    static constexpr bool PAIR_WANTED = false;
+#elif defined(MPCG_PAIR_ALL)
+    static constexpr bool PAIR_WANTED = true;
+#else
+    static constexpr bool PAIR_WANTED = FCONST;
+#endif
+    static constexpr bool PAIR_CHAINS = PAIR_WANTED && CHAIN_SPLIT && (N_ + 1) / 2 * NX_ * NX_ <= (N_ + 1) * NDH &&
+                                        (N_ + 1) / 2 * NX_ <= 128;
     // branch-free Riccati step (every lane, prefetch after the pivot reads, pivot failures
     // voted from a register)
     static constexpr bool FAC_FLAT = !COMPACT || MPCG_C3_FACFLAT;
@@ -1382,11 +1396,70 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     STAMP_LAP(6);
                     double* const pch = &S.bx[0][0];
                     static_assert((N + 1) * NZ >= N * NX, "chain storage");
+                    // Two-stage composed maps (PAIR): p_k = (h_k + G_k h_{k+1}) + G_k G_{k+1} p_{k+2}
+                    // on the stages k = N-2, N-4, ... (the chain), then p_k = h_k + G_k p_{k+1} on the
+                    // others, all at once; the forward map likewise (dx_{o+1} = Phi_o Phi_{o-1} dx_{o-1}
+                    // + Phi_o e_{o-1} + e_o on odd o, then the even stages).  Half the sequential
+                    // steps; each composition needs the partner stage's whole map, exchanged
+                    // through the barrier-term rows and the pivot scratch, both dead from the
+                    // Riccati step to the next barrier pass (which rewrites every barrier entry
+                    // but the always-zero slot, restored after the forward pass).
+                    constexpr bool PAIR = C::PAIR_CHAINS;
+                    constexpr int NSLOT = (N + 1) / 2;  // slots k >> 1 of the publishing stages k <= N - 1
+                    double* const XG = &S.dH[0][0];
+                    double* const Xh = &S.Msc[0];
+                    static_assert(!PAIR || (NSLOT * NX * NX <= (N + 1) * C::NDH && NSLOT * NX <= 128),
+                                  "pair exchange storage");
+                    // the stage's rows of (M, v) to its exchange slot / composed with the partner's slot
+                    auto publish = [&](int sl, const double (&M)[RS][NX], const double (&v)[RS]) {
+#pragma unroll
+                        for (int t = 0; t < RS; ++t) {
+                            if (!rv[t]) continue;
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) XG[(sl * NX + rs[t]) * NX + j] = M[t][j];
+                            Xh[sl * NX + rs[t]] = v[t];
+                        }
+                    };
+                    auto compose = [&](int sl, double (&M)[RS][NX], double (&v)[RS]) {
+                        double M2[RS][NX], v2[RS];
+#pragma unroll
+                        for (int t = 0; t < RS; ++t) {
+                            v2[t] = v[t];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) M2[t][j] = 0.0;
+                        }
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) {
+                            const double hm = Xh[sl * NX + m];
+                            double xr[NX];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) xr[j] = XG[(sl * NX + m) * NX + j];
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                v2[t] += M[t][m] * hm;
+#pragma unroll
+                                for (int j = 0; j < NX; ++j) M2[t][j] += M[t][m] * xr[j];
+                            }
+                        }
+#pragma unroll
+                        for (int t = 0; t < RS; ++t) {
+                            v[t] = v2[t];
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) M[t][j] = M2[t][j];
+                        }
+                    };
+                    // backward: the stages k = N-1, N-3, ... publish, k = N-2, N-4, ... compose
+                    const bool bfix = k >= 1 && k <= N - 1 && ((N - 1 - k) & 1) == 0;
+                    if constexpr (PAIR) {
+                        if (bfix) publish(k >> 1, Gr, hr);
+                        wave_sync();
+                        if (k >= 1 && k <= N - 2 && ((N - k) & 1) == 0) compose((k + 1) >> 1, Gr, hr);
+                    }
                     double pu[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) pu[i] = S.q[N][NU + i];
                     #pragma unroll
-                    for (int kk = N - 1; kk >= 1; --kk) {  // p_0 is not needed
+                    for (int kk = PAIR ? N - 2 : N - 1; kk >= 1; kk -= PAIR ? 2 : 1) {  // p_0 is not needed
                         double pn[RS];
 #pragma unroll
                         for (int t = 0; t < RS; ++t) {
@@ -1424,6 +1497,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int i = 0; i < NX; ++i) pu[i] = readlane_d(pn[i / PARTS], kk * PARTS + i % PARTS);
                     }
                     wave_sync();
+                    if constexpr (PAIR) {
+                        // the stages between the chain's: one map applied to the recorded p_{k+1}
+                        if (bfix) {
+                            const double* src = (k + 1 < N) ? pch + (k + 1) * NX : &S.q[N][NU];
+                            double pnx[NX];
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) pnx[i] = src[i];
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                double a = hr[t];
+#pragma unroll
+                                for (int j = 0; j < NX; ++j) a += Gr[t][j] * pnx[j];
+                                if (rv[t]) pch[k * NX + rs[t]] = a;
+                            }
+                        }
+                        wave_sync();
+                    }
                     double pmine[NX];
                     {
                         const double* src = (kv + 1 < N) ? pch + (kv + 1) * NX : &S.q[N][NU];
@@ -1458,12 +1548,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         for (int u = 0; u < NU; ++u) acc += Fat(kv, rs[t], u) * kf[u];
                         ec[t] = acc;
                     }
+                    // forward: the even stages publish (Phi_k, e_k), the odd stages compose
+                    const bool ffix = k <= N - 1 && (k & 1) == 0;
+                    if constexpr (PAIR) {
+                        if (ffix) publish(k >> 1, Gc, ec);
+                        wave_sync();
+                        if (k >= 1 && k <= N - 1 && (k & 1)) compose(k >> 1, Gc, ec);
+                    }
                     // dx_{kk+1} goes straight to its place in the QP step, ddz[kk + 1]
                     double dxu[NX];
 #pragma unroll
                     for (int i = 0; i < NX; ++i) dxu[i] = 0.0;
                     #pragma unroll
-                    for (int kk = 0; kk < N; ++kk) {
+                    for (int kk = PAIR ? 1 : 0; kk < N; kk += PAIR ? 2 : 1) {
                         double dn[RS];
 #pragma unroll
                         for (int t = 0; t < RS; ++t) {
@@ -1493,12 +1590,31 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int t = 0; t < RS; ++t)
                                 if (rv[t]) S.ddz[kk + 1][NU + rs[t]] = dn[t];
                         }
-                        if (kk + 1 < N) {
+                        if (kk + (PAIR ? 2 : 1) < N) {
 #pragma unroll
                             for (int i = 0; i < NX; ++i) dxu[i] = readlane_d(dn[i / PARTS], kk * PARTS + i % PARTS);
                         }
                     }
                     wave_sync();
+                    if constexpr (PAIR) {
+                        // the even stages: one map applied to the recorded dx_k
+                        if (ffix) {
+                            double dxs[NX];
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) dxs[i] = k >= 1 ? S.ddz[k][NU + i] : 0.0;
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                double a = ec[t];
+#pragma unroll
+                                for (int j = 0; j < NX; ++j) a += Gc[t][j] * dxs[j];
+                                if (rv[t]) S.ddz[k + 1][NU + rs[t]] = a;
+                            }
+                        }
+                        // the barrier rows' always-zero slot, overwritten by the exchange (the
+                        // rest of the rows is rewritten by the next predictor's barrier pass)
+                        for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
+                        wave_sync();
+                    }
                     STAMP_LAP(9);
                     if (own) {
                         double dxm[NX], dxn[NX], du[NU];
