@@ -193,6 +193,10 @@ struct Lds {
     double H[GFH ? 1 : N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
     double g[N + 1][NZ];
     double F[GFH ? 1 : N][C::NFR][C::NFC];  // [B A] (C::COMPACT: rows x+ y+ psi+ s+, no slack column)
+    // GFH: the Riccati step's copy of the next stage's blocks (one coalesced global load per
+    // lane per stage instead of a gather per entry)
+    double Fst[GFH && !C::COMPACT ? C::NFR : 1][C::NFC];
+    double Hst[GFH && !C::COMPACT ? C::NHP : 1];
     double b[N][NX];          // shooting defects
     double dH[N + 1][C::NDH]; // barrier terms: diag(nz) + h-row block (column-major packed), last = 0
     double q[N + 1][NZ];      // Newton gradient
@@ -563,31 +567,33 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // the s+ row's coefficients of a and v (uniform, bit-identical to erk_unicycle's)
     double srow_a = 0.0, srow_v = 0.0;
     if constexpr (C::FCONST) erk_srow(pr, srow_a, srow_v);
-    auto Fat = [&](int kq, int m, int j) -> double {
+    auto FatB = [&](const double (*Fk)[C::NFC], int m, int j) -> double {
         if constexpr (C::FCONST) {
             // rows psi+, v+, s+ (, slack+) are constants (z = [a w x y psi v s (slack)])
             if (m == 2) return j == 1 ? pr.dt : (j == 4 ? 1.0 : 0.0);
             if (m == 3) return j == 0 ? pr.dt : (j == 5 ? 1.0 : 0.0);
             if (m == 4) return j == 0 ? srow_a : (j == 5 ? srow_v : (j == 6 ? 1.0 : 0.0));
             if (m >= 5) return j == NU + m ? 1.0 : 0.0;
-            return Fb(kq)[m][j];
+            return Fk[m][j];
         } else if constexpr (C::COMPACT) {
             if (m == 3) return j == bike::ZV ? 1.0 : (j == bike::ZA ? pr.dt : 0.0);
             if (m == 4) return j == bike::ZDELTA ? 1.0 : (j == bike::ZW ? pr.dt : 0.0);
             if (j == ZS) return 0.0;
-            return Fb(kq)[m < 3 ? m : 3][j < ZS ? j : j - 1];
+            return Fk[m < 3 ? m : 3][j < ZS ? j : j - 1];
         } else {
-            return Fb(kq)[m][j];
+            return Fk[m][j];
         }
     };
-    auto Hat = [&](int kq, int i, int j) -> double {
+    auto HatB = [&](const double* Hk, int i, int j) -> double {
         if constexpr (C::COMPACT) {
-            if (i == ZS || j == ZS) return (i == j) ? Hb(kq)[C::NHP - 1] : 0.0;
-            return Hb(kq)[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
+            if (i == ZS || j == ZS) return (i == j) ? Hk[C::NHP - 1] : 0.0;
+            return Hk[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
         } else {
-            return Hb(kq)[sym(i, j)];
+            return Hk[sym(i, j)];
         }
     };
+    auto Fat = [&](int kq, int m, int j) -> double { return FatB(Fb(kq), m, j); };
+    auto Hat = [&](int kq, int i, int j) -> double { return HatB(Hb(kq), i, j); };
     // dynamics residual b + F dz - dz+ of stage kq at the current QP iterate (same operation order
     // as the residual phase, which stores it unless C::COMPACT)
     auto rdyn_at = [&](int kq, int i) -> double {
@@ -1136,6 +1142,29 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         if constexpr (C::COMPACT) return Hat(kq, ei, ej);
                         else return Hb(kq)[le];
                     };
+                    // GFH: stage kn's blocks come from the staging copy (written this step from the
+                    // coalesced loads issued one step earlier)
+                    auto HelS = [&]() -> double {
+                        if constexpr (C::COMPACT) return HatB(S.Hst, ei, ej);
+                        else return S.Hst[le];
+                    };
+                    // measured: C4 53.40 -> 52.82 ms with the staging copy, C3 21.01 -> 21.67 (its
+                    // compact blocks are rebuilt entry by entry and the copy adds live state): C4 only
+#ifdef MPCG_NO_STAGE
+                    constexpr bool STG = false;  // A/B: the Riccati step reads the global blocks directly
+#else
+                    constexpr bool STG = GFH && !C::COMPACT;
+#endif
+                    constexpr int NFB = C::NFR * C::NFC;
+                    static_assert(!GFH || (NFB <= 64 && C::NHP <= 64), "one staged entry per lane");
+                    double gsf = 0.0, gsh = 0.0;  // the staged entries of the next block in flight
+                    auto stage_load = [&](int kq) {
+                        if constexpr (STG) {
+                            gsf = lane < NFB ? gF[(size_t)kq * NFB + lane] : 0.0;
+                            gsh = lane < C::NHP ? gH[(size_t)kq * C::NHP + lane] : 0.0;
+                        }
+                    };
+                    if (N >= 2) stage_load(N - 2);
                     hv = Hel(N - 1) + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
 #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
@@ -1148,11 +1177,24 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         // block's reads (off the recursion's critical path, and not in front of
                         // the LDS traffic the next step waits for)
                         const int kn = kk > 0 ? kk - 1 : 0;
+                        if constexpr (STG) {
+                            // stage kn's blocks into the staging copy, then the loads of kn - 1
+                            if (lane < NFB) (&S.Fst[0][0])[lane] = gsf;
+                            if (lane < C::NHP) S.Hst[lane] = gsh;
+                            wave_sync();
+                            if (kk >= 2) stage_load(kk - 2);
+                        }
                         double fi2[NX], fj2[NX], hv2;
                         auto prefetch = [&]() {
+                            if constexpr (STG) {
 #pragma unroll
-                            for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
-                            hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
+                                for (int m = 0; m < NX; ++m) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
+                                hv2 = HelS() + S.dH[kn][dhd] + S.dH[kn][dhb];
+                            } else {
+#pragma unroll
+                                for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
+                                hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
+                            }
                         };
                         if constexpr (!FAC_FLAT) prefetch();
                         double v = hv;
