@@ -17,9 +17,12 @@ Scene data is uploaded once before the timed region (inputs resident in HBM).
     python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  `roofline` prices the solve kernel against HBM
-with SURVEY.md §8(d)'s algorithmic bytes per solve (the path is fp64-VALU /
-latency bound); `roofline.traffic` comes from the rocprofv3 PMC
+Rank 0 prints one JSON line.  `roofline` prices the solve kernel against the
+fp64 vector peak with the algorithm's analytic operation count
+(oscar_mpc_planner_mr_modification_amd/flopmodel.py, times the SQP and IPM
+iterations each solve executed; the path is fp64-latency bound, DESIGN.md §3);
+`roofline.hbm` prices it against HBM with SURVEY.md §8(d)'s algorithmic bytes
+per solve; `roofline.traffic` comes from the rocprofv3 PMC
 summary under profiles/ only when that summary was taken on the same kernel
 sources (source hash), else it is null.  `cpu_baseline` times the C oracle
 (same algorithm, OpenMP over solves) on a bounded sample of the same batch
@@ -416,24 +419,35 @@ def main():
     value = args.steps * B * world / elapsed
     exit_h, xt_h, info_h = (wl.out[k].cpu().numpy() for k in ("exit", "xtraj", "info"))
 
+    # roofline: the solve is fp64-latency bound, so it is priced against the fp64
+    # vector peak with the ALGORITHM's operations (flopmodel.py: analytic counts per SQP and IPM
+    # iteration, times the iterations each solve of this batch executed); HBM stays a secondary
+    # figure with SURVEY.md §8(d)'s algorithmic bytes per solve
+    from oscar_mpc_planner_mr_modification_amd import flopmodel
+
+    flop = float(flopmodel.solve_ops(lay, info_h).sum())
+    tflops = flop / (kern_ms * 1e-3) / 1e12
     bps = algorithmic_bytes_per_solve(lay)
     achieved = bps * B / (kern_ms * 1e-3) / 1e9
     traffic, f64, counters = load_counters(args.traffic_json, args.config, B)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sqp_kernel",
-                "kernel_ms": round(kern_ms, 4), "bytes_per_solve": bps, "counters": counters}
+    roofline = {"bound": "fp64_valu", "achieved": round(tflops, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": tflops / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
+                "kernel": "sqp_kernel", "kernel_ms": round(kern_ms, 4),
+                "flop_per_solve": round(flop / B), "flop_model": "analytic (flopmodel.py) x executed iterations",
+                "hbm": {"achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "bytes_per_solve": bps, "traffic": traffic},
+                "counters": counters}
     if f64:
-        # the path is fp64-VALU / latency bound: issued fp64 FLOP/s of the solve kernel
-        # (PMC SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) against the vector peak, and
-        # the useful share: issued x the VALU lane utilisation (rocprofv3 VALUUtilization, the
-        # kernel's average active-lane fraction, applied to its fp64 instructions)
+        # cross-check from the PMC pass on the same sources: issued fp64 FLOP/s of the solve kernel
+        # (SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) and that figure weighted by the
+        # kernel's VALU lane utilisation (rocprofv3 VALUUtilization)
         tf = f64["flop"] / (kern_ms * 1e-3) / 1e12
         roofline["fp64_valu_issued"] = {"achieved_tflops": round(tf, 3), "peak_tflops": FP64_VALU_PEAK_TFLOPS,
                                         "frac": tf / FP64_VALU_PEAK_TFLOPS}
         if f64.get("lane_util"):
             lu = f64["lane_util"]
-            roofline["fp64_valu_useful"] = {"achieved_tflops": round(tf * lu, 3), "lane_util": round(lu, 4),
-                                            "frac": tf * lu / FP64_VALU_PEAK_TFLOPS}
+            roofline["fp64_valu_lane_weighted"] = {"achieved_tflops": round(tf * lu, 3), "lane_util": round(lu, 4),
+                                                   "frac": tf * lu / FP64_VALU_PEAK_TFLOPS}
     if "prepare" in phase_ms and hasattr(wl, "producer_roofline"):
         roofline["producer"] = wl.producer_roofline(phase_ms["prepare"])
     ok = exit_h == 1

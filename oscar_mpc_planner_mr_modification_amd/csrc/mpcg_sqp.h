@@ -129,7 +129,11 @@ struct Cfg {
     // per-CU line (JS 47.2 -> 39.9 KB, 365.8k -> 459.6k solves/s).  The other instances keep all
     // rows: C4 stays above the line either way (it measured 2.6 % slower with them constant) and
     // on N 20 the constant rows changed the register allocation into scratch (C2 0 -> 128 B/lane)
+#ifdef MPCG_FCONST_ALL
+    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30;  // A/B: C4 (12 obstacles) too
+#else
     static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30 && NE_ <= 8;
+#endif
     static constexpr int NFR = COMPACT ? 4 : (FCONST ? 2 : NX), NFC = COMPACT ? NZ - 1 : NZ;
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // the vector chains split over the parts of a stage (rows of the backward map, columns of
@@ -151,7 +155,7 @@ struct Cfg {
 #elif defined(MPCG_PAIR_ALL)
     static constexpr bool PAIR_WANTED = true;
 #else
-    static constexpr bool PAIR_WANTED = FCONST;
+    static constexpr bool PAIR_WANTED = FCONST && NE_ <= 8;
 #endif
     static constexpr bool PAIR_CHAINS = PAIR_WANTED && CHAIN_SPLIT && (N_ + 1) / 2 * NX_ * NX_ <= (N_ + 1) * NDH &&
                                         (N_ + 1) / 2 * NX_ <= 128;
