@@ -126,14 +126,12 @@ struct Cfg {
     // slack) of [B A] are the same constants at every stage (RK4 integrates them exactly,
     // erk_srow): on the long horizons with few obstacles only the x+ and y+ rows are stored,
     // which (with the LEAN storage) brings N 30 with 4 or 5 obstacles under the four-solves-
-    // per-CU line (JS 47.2 -> 39.9 KB, 365.8k -> 459.6k solves/s).  The other instances keep all
-    // rows: C4 stays above the line either way (it measured 2.6 % slower with them constant) and
-    // on N 20 the constant rows changed the register allocation into scratch (C2 0 -> 128 B/lane)
-#ifdef MPCG_FCONST_ALL
-    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30;  // A/B: C4 (12 obstacles) too
-#else
-    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30 && NE_ <= 8;
-#endif
+    // per-CU line (JS 47.2 -> 39.9 KB, 365.8k -> 459.6k solves/s).  C4 (12 obstacles) stays above
+    // the line either way and keeps its blocks in the global workspace (GFH), where the constant
+    // rows shrink the per-solve block 15.3 -> 10.3 KB: 52.85 -> 51.26 ms, 304.5k -> 314.0k solves/s
+    // (profiles/r02v_ab_*_C4.json; at three solves per CU, before GFH, it was 2.6 % slower).  On
+    // N 20 the constant rows changed the register allocation into scratch (C2 0 -> 128 B/lane).
+    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30;
     static constexpr int NFR = COMPACT ? 4 : (FCONST ? 2 : NX), NFC = COMPACT ? NZ - 1 : NZ;
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // the vector chains split over the parts of a stage (rows of the backward map, columns of

@@ -6,10 +6,13 @@ RTI and interior-point iteration counts on both sides) also within 1e-4.
 
 C5 exception: the SH-MPC slack state is pinned at 0 by the x0
 bound and its zero dynamics (generate_acados_solver.py:95, solver_model.py:289-292),
-so its lower-bound rows have zero gap at every stage.  On a few QPs the interior
-point stalls on the central path and the Riccati pivot's sign is then decided by
-rounding; such a solve ends in a QP NaN status on one side.  The test bounds their
-number and checks that every disagreement is of that kind."""
+so its lower-bound rows have zero gap at every stage and the QP is dual-degenerate
+(the pinned rows' multipliers and the slack's dynamics multipliers trade along an
+unbounded ray).  On a few QPs the interior point drifts along that ray until the
+multipliers reach 1e13-1e15 and the residuals' rounding floor (one ulp of them) passes
+the tolerance; whether it converges first is decided by rounding, and the solve then
+ends in a QP NaN status on one side.  The test bounds their number and checks that
+every disagreement is of that kind."""
 import os
 import sys
 
