@@ -77,10 +77,12 @@ def gather_winners(records, world: int, out=None, group=None, total: int | None 
         send[:records.shape[0]] = records
         buf = torch.empty((per * world, width), dtype=records.dtype, device=records.device)
     if dist.get_backend(group) == "gloo":
-        parts = list(buf.chunk(world, 0))
-        dist.all_gather(parts, send, group=group)
-        if parts[0].data_ptr() != buf.data_ptr():
-            buf.copy_(torch.cat(parts, 0))
+        # gloo all-gathers host tensors: device blocks are staged through the host (the
+        # rehearsal of the multi-rank path on one GPU, bench.py MPCG_BENCH_BACKEND=gloo)
+        send_h = send.cpu()
+        parts = [torch.empty_like(send_h) for _ in range(world)]
+        dist.all_gather(parts, send_h, group=group)
+        buf.copy_(torch.cat(parts, 0))
     else:
         dist.all_gather_into_tensor(buf, send, group=group)
     if counts is None:
@@ -91,3 +93,17 @@ def gather_winners(records, world: int, out=None, group=None, total: int | None 
         out.copy_(res)
         return out
     return res
+
+
+def all_reduce_(t, op, group=None):
+    """In-place all-reduce of `t` (any device); under gloo the tensor is staged through
+    the host, as gloo reduces host tensors."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "gloo" and t.device.type != "cpu":
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
