@@ -254,13 +254,15 @@ class ShmpcWorkload(Workload):
                                     [20251212] * len(chunks), [first + int(c[0]) for c in chunks]))
             self.scenes = ScenarioScenes(stage_params=np.concatenate([q.stage_params for q in parts]),
                                          state=np.concatenate([q.state for q in parts]),
-                                         samples=np.concatenate([q.samples for q in parts]), n_solvers=P)
+                                         samples=np.concatenate([q.samples for q in parts]), n_solvers=P,
+                                         main_warm=np.concatenate([q.main_warm for q in parts]))
             del parts
         else:
             self.scenes = make_shmpc_scenes(lay, S, P, self.n_obs, self.n_samples, first_scene=first)
         self.gen_s = time.time() - t0
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_sp, self.d_st, self.d_smp = t(self.scenes.stage_params), t(self.scenes.state), t(self.scenes.samples)
+        self.d_mw = t(self.scenes.main_warm)   # the main solver's previous plan (scenario.previous_plan)
         self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
         B = self.B
         f64 = dict(dtype=torch.float64, device=dev)
@@ -287,7 +289,7 @@ class ShmpcWorkload(Workload):
         if ev:
             ev[0].record(s)
         native.prepare_scenario_device(self.pr, self.P, self.d_sp, self.d_st, self.d_smp, self.radius, DECELERATION,
-                                       out=self.prep, stream=s)
+                                       main_warm=self.d_mw, out=self.prep, stream=s)
         if ev:
             ev[1].record(s)
         native.solve_batch_device(self.pr, self.prep["params"], self.prep["warm"], self.prep["xinit"], out=self.out,
@@ -312,15 +314,17 @@ class ShmpcWorkload(Workload):
 
         n = min(n_scenes, self.S)
         sub = ScenarioScenes(stage_params=self.scenes.stage_params[:n], state=self.scenes.state[:n],
-                             samples=self.scenes.samples[:n * self.P], n_solvers=self.P)
+                             samples=self.scenes.samples[:n * self.P], n_solvers=self.P,
+                             main_warm=self.scenes.main_warm[:n])
         hb = prepare_scenario_host(self.lay, sub, self.radius, DECELERATION)
         prm, wrm, _ = self.host_inputs(0, n * self.P)
         return max(float(np.abs(hb.params - prm).max()), float(np.abs(hb.warm - wrm).max()))
 
     def producer_roofline(self, prep_ms):
         lay, N = self.lay, self.lay.N
-        # the producer reads every sample once and streams the solver inputs out
+        # the producer reads every sample and the previous plan once and streams the solver inputs out
         prep_bytes = self.B * ((N - 1) * self.n_obs * self.n_samples * 16 + N * lay.npar * 8 + (N + 1) * lay.nvar * 8)
+        prep_bytes += self.S * (N + 1) * lay.nvar * 8
         gbs = prep_bytes / (prep_ms * 1e-3) / 1e9
         return {"kernel": "scenario_prepare_kernel", "kernel_ms": round(prep_ms, 4), "algorithmic_gbs": round(gbs, 2),
                 "frac": gbs / HBM_PEAK_GBS}

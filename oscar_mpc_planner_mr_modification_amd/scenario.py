@@ -28,8 +28,19 @@ slack stays at its initial value over the horizon and the scenario rows act
 as hard constraints; a copy whose halfspaces are contradictory ends in a QP
 failure, and the pick below takes another copy.
 
+Warm start: the main solver's previous plan, shifted (Solver::initializeWarmstart,
+acados_solver_interface.cpp:286-301), which the copies inherit.  In steady operation
+that plan satisfied the previous step's scenario rows, so it keeps clear of the
+obstacles' sample clouds; the stand-in is a kinematically tracked trajectory pushed
+PLAN_CLEAR from every obstacle's mean path (synthetic._guess_trajectory, the C2
+generator's guidance stand-in), the best of PLAN_TRIES passing patterns.  With the
+braking plan instead (`previous_plan=False`; the reference's start-up and
+after-failure case) a plan through an obstacle's sample cloud gives halfspaces
+pointing every way around it, an empty polygon and an infeasible first QP.
+
 Seeds: scene i uses `seed + i`; parallel solver s draws its samples from
-`seed + i` with stream s, so any sub-range regenerates bit-identically.
+`seed + i` with stream s and the previous plan's passing patterns come from stream
+0, so any sub-range regenerates bit-identically.
 """
 from __future__ import annotations
 
@@ -38,13 +49,19 @@ from dataclasses import dataclass
 import numpy as np
 
 from .layouts import Layout
-from .synthetic import DECELERATION, OBSTACLE_RADIUS, ROBOT_RADIUS, SETTINGS_WEIGHTS, _path, _path_eval
+from .synthetic import (DECELERATION, OBSTACLE_RADIUS, ROBOT_RADIUS, SETTINGS_WEIGHTS, _guess_trajectory, _path,
+                        _path_eval)
 
 SEED0 = 20251212
 SLACK_WEIGHT = 10000.0        # settings.yaml:89
 PARALLEL_SOLVERS = 4          # settings.yaml:48-49
 SAMPLE_VEL_STD = 0.3          # [m/s] per-axis velocity noise integrated over the horizon
 DUMMY_B = 100.0               # inactive stage-0 rows
+# previous plan: clearance from the obstacle means = robot + obstacle radius + ~2.5 sigma of
+# the samples' spread at the last stage (SAMPLE_VEL_STD * dt * sqrt(N))
+PLAN_CLEAR = ROBOT_RADIUS + OBSTACLE_RADIUS + 0.65
+PLAN_TRIES = 8
+SPAWN_AHEAD, SPAWN_LAT = 16.0, 4.0
 
 
 @dataclass
@@ -101,14 +118,47 @@ def reduce_samples(samples: np.ndarray, ref: np.ndarray, n_constraints: int, rad
     return out
 
 
+def previous_plan(layout: Layout, x0: np.ndarray, path, obstacles, rng) -> np.ndarray:
+    """(N+1, nu+nx) warm start [a w | x y psi v s slack] along a collision-free tracked
+    trajectory from x0 (stage 0 = x0, inputs inside their bounds, slack 0)."""
+    N, dt = layout.N, layout.dt
+    n_obs = len(obstacles)
+    best = None
+    signs = [1 if (j % 2) == 0 else -1 for j in range(n_obs)]
+    for _ in range(PLAN_TRIES):
+        pos, vel, clear = _guess_trajectory(x0[:5], path, obstacles, signs, N, dt,
+                                            SETTINGS_WEIGHTS["reference_velocity"], clear=PLAN_CLEAR)
+        if best is None or clear > best[2]:
+            best = (pos, vel, clear)
+        if clear >= PLAN_CLEAR - 0.15:
+            break
+        signs = list(rng.choice([-1, 1], n_obs))
+    pos, vel = best[0], best[1]
+    speed = np.hypot(vel[:, 0], vel[:, 1])
+    psi = np.unwrap(np.concatenate([[x0[2]], np.arctan2(vel[1:, 1], vel[1:, 0])]))
+    seg = np.hypot(*np.diff(pos, axis=0).T)
+    warm = np.zeros((N + 1, layout.nvar))
+    warm[:, 2:4] = pos
+    warm[:, 4] = psi
+    warm[:, 5] = speed
+    warm[:, 6] = x0[4] + np.concatenate([[0.0], np.cumsum(seg)])
+    warm[0, 2:7] = x0[:5]
+    warm[:N, 0] = np.clip(np.diff(warm[:, 5]) / dt, -2.0, 2.0)
+    warm[:N, 1] = np.clip(np.diff(warm[:, 4]) / dt, -0.8, 0.8)
+    warm[N, 0:2] = warm[N - 1, 0:2]
+    return warm
+
+
 def make_shmpc_scenes(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
-                      n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioScenes:
+                      n_samples: int = 100, seed: int = SEED0, first_scene: int = 0,
+                      previous_plan_warm: bool = True) -> ScenarioScenes:
     assert layout.model == "unicycle_slack" and layout.n_scen > 0
     N, dt, npar, ix = layout.N, layout.dt, layout.npar, layout.idx
     S, P, M = n_scenes, n_solvers, n_obs * n_samples
     stage_params = np.zeros((S, npar))
     state = np.zeros((S, layout.nx))
     samples = np.zeros((S * P, N, M, 2))
+    main_warm = np.zeros((S, N + 1, layout.nvar)) if previous_plan_warm else None
     tk = dt * np.arange(N)
     for sc in range(S):
         rng = np.random.default_rng(seed + first_scene + sc)
@@ -122,8 +172,8 @@ def make_shmpc_scenes(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_S
         state[sc, :5] = (ego_pos[0], ego_pos[1], psi0, v0, s_ego)
         means = np.zeros((n_obs, N, 2))
         for j in range(n_obs):
-            ahead = rng.uniform(2.0, 10.0)
-            lat = rng.uniform(-3.0, 3.0)
+            ahead = rng.uniform(2.0, SPAWN_AHEAD)
+            lat = rng.uniform(-SPAWN_LAT, SPAWN_LAT)
             pj, tj = _path_eval(coef, starts, s_ego + ahead)
             nj = np.array([-tj[1], tj[0]])
             vj = rng.normal(0.0, 0.7, size=2)
@@ -147,7 +197,11 @@ def make_shmpc_scenes(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_S
             walk = np.cumsum(vel * dt, axis=2)
             smp = means[:, None] + walk                      # (n_obs, n_samples, N, 2)
             samples[sc * P + s] = smp.transpose(2, 0, 1, 3).reshape(N, M, 2)
-    return ScenarioScenes(stage_params=stage_params, state=state, samples=samples, n_solvers=P)
+        if main_warm is not None:
+            obstacles = [(means[j, 0], (means[j, 1] - means[j, 0]) / dt) for j in range(n_obs)]
+            main_warm[sc] = previous_plan(layout, state[sc], (coef, starts, s_ego), obstacles,
+                                          np.random.default_rng([seed + first_scene + sc, 0]))
+    return ScenarioScenes(stage_params=stage_params, state=state, samples=samples, n_solvers=P, main_warm=main_warm)
 
 
 def prepare_scenario_host(layout: Layout, sc: ScenarioScenes, radius: float = ROBOT_RADIUS + OBSTACLE_RADIUS,

@@ -163,7 +163,7 @@ def _min_clearance(pos, opos, ovel, dt):
     return m
 
 
-def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
+def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref, clear=None):
     """A collision-free, kinematically consistent guidance trajectory (stand-in for the
     external guidance_planner's space-time PRM output): nominal progress along the
     path towards v_ref, a lateral offset that passes obstacle j on side signs[j]
@@ -172,7 +172,8 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
     bounds from the current state (guidance_planner's search starts from the robot's
     state and only returns collision-free trajectories).
     Returns positions and velocities at t = k*dt, k = 0..N, and the smallest clearance
-    of the stage samples from the obstacles (the constraints' and the physical time)."""
+    of the stage samples from the obstacles (the constraints' and the physical time).
+    `clear`: the clearance the desired path is pushed out to (default GUIDE_CLEAR + 0.3)."""
     coef, starts, s_ego = tangent_path
     CLEAR = 0.8
     fine = np.linspace(0, N * dt, 8 * N + 1)
@@ -197,7 +198,7 @@ def _guess_trajectory(ego, tangent_path, obstacles, signs, N, dt, vref):
     if obstacles:
         opos = np.array([o[0] for o in obstacles])
         ovel = np.array([o[1] for o in obstacles])
-        desired = _clear_path(desired, fine, opos, ovel, dt, GUIDE_CLEAR + 0.3)
+        desired = _clear_path(desired, fine, opos, ovel, dt, GUIDE_CLEAR + 0.3 if clear is None else clear)
     # track the desired path with a pure-pursuit unicycle inside the input
     # bounds (|a| <= 2, |w| <= 0.8), so the guess is kinematically reachable
     # from the current state, as guidance_planner's start-state-aware search is

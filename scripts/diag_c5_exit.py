@@ -20,7 +20,8 @@ dev = torch.device("cuda:0")
 sc = make_shmpc_scenes(lay, S)
 t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
 pr = native.problem_from_layout(lay)
-inp = native.prepare_scenario_device(pr, 4, t(sc.stage_params), t(sc.state), t(sc.samples), 0.65, 3.0)
+inp = native.prepare_scenario_device(pr, 4, t(sc.stage_params), t(sc.state), t(sc.samples), 0.65, 3.0,
+                                     main_warm=t(sc.main_warm))
 out = native.solve_batch_device(pr, inp["params"], inp["warm"], inp["xinit"])
 torch.cuda.synchronize()
 g = {k: v.cpu().numpy() for k, v in out.items()}

@@ -40,7 +40,7 @@ def test_scenario_producer_bit_exact(dev, cfg, n_obs, n_samples):
     from oscar_mpc_planner_mr_modification_amd.layouts import config_layout, safe_horizon_layout
     from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_scenes, prepare_scenario_host
     lay = config_layout("C5") if cfg == "C5" else safe_horizon_layout(N=10, n_constraints=4)
-    sc = make_shmpc_scenes(lay, 6, n_obs=n_obs, n_samples=n_samples, seed=77)
+    sc = make_shmpc_scenes(lay, 6, n_obs=n_obs, n_samples=n_samples, seed=77, previous_plan_warm=False)
     # exact ties: duplicate one solver's stage-3 samples
     sc.samples[1, 3, 5:10] = sc.samples[1, 3, 0:5]
     ref = prepare_scenario_host(lay, sc, 0.65, 3.0)

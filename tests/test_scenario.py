@@ -80,3 +80,32 @@ def test_codegen_model_map_has_slack(tmp_path):
     m = model_map(lay)
     assert m["slack"] == ["x", 7, 0.0, 5000.0]
     assert solver_settings(lay) == {"N": 20, "nx": 6, "nu": 2, "nvar": 8, "npar": 127}
+
+
+def test_previous_plan_warm_start():
+    """The C5 copies start from the main solver's previous plan (scenario.previous_plan):
+    stage 0 is the robot state, inputs inside their bounds, the slack state 0; the samples
+    do not depend on the warm-start choice."""
+    from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_scenes
+    lay = config_layout("C5")
+    sc = make_shmpc_scenes(lay, 24, seed=31)
+    w = sc.main_warm
+    assert w.shape == (24, lay.N + 1, lay.nvar)
+    np.testing.assert_array_equal(w[:, 0, 2:7], sc.state[:, :5])
+    assert np.abs(w[:, :, 0]).max() <= 2.0 and np.abs(w[:, :, 1]).max() <= 0.8
+    assert np.all(w[:, :, 7] == 0.0) and np.all(w[:, :, 5] >= 0.0)
+    brk = make_shmpc_scenes(lay, 24, seed=31, previous_plan_warm=False)
+    assert brk.main_warm is None
+    np.testing.assert_array_equal(brk.samples, sc.samples)
+
+
+def test_c5_workload_success(oracle_mod):
+    """The round-2 C5 workload (sparser obstacle field, previous-plan warm start): most
+    copies succeed and most scenes have a successful copy (measured on the full batch:
+    DESIGN.md §3.2)."""
+    lay = config_layout("C5")
+    b = make_shmpc_batch(lay, 32, seed=20251212)
+    r = oracle_mod.Oracle(lay).solve_batch(b.params, b.warm, b.xinit, nthreads=4)
+    st = r["status"].reshape(32, 4)
+    assert (st == 1).mean() >= 0.8
+    assert (st == 1).any(1).mean() >= 0.8
