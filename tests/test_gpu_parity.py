@@ -93,8 +93,9 @@ def test_parity_shmpc_slack_model(native, torch_dev, oracle_mod, N, n_scen, n_sc
     got = {k: v.cpu().numpy() for k, v in out.items()}
     assert got["xtraj"].shape == (len(b.xinit), N + 1, 6)
     _compare(ref, got, f"C5 N={N} scen={n_scen}")
-    assert np.array_equal(select_lowest_cost(got["pobj"], got["exit"], b.n_solvers),
-                          select_lowest_cost(ref["pobj"], ref["status"], b.n_solvers))
+    from conftest import picks_equivalent
+    assert picks_equivalent(select_lowest_cost(got["pobj"], got["exit"], b.n_solvers),
+                            select_lowest_cost(ref["pobj"], ref["status"], b.n_solvers), ref["pobj"])
 
 
 @pytest.mark.parametrize("N,n_dec,n_scenes,seed", [(30, 12, 48, 20251212), (10, 4, 16, 9)])

@@ -93,7 +93,7 @@ def test_shmpc_pipeline_matches_oracle(dev, oracle_mod):
     ref = oracle_mod.Oracle(lay).solve_batch(hb.params, hb.warm, hb.xinit)
     pr = native.problem_from_layout(lay)
     inp = native.prepare_scenario_device(pr, sc.n_solvers, _t(sc.stage_params, dev), _t(sc.state, dev),
-                                         _t(sc.samples, dev), 0.65, 3.0)
+                                         _t(sc.samples, dev), 0.65, 3.0, main_warm=_t(sc.main_warm, dev))
     out = native.solve_batch_device(pr, inp["params"], inp["warm"], inp["xinit"])
     best = native.select_lowest_cost_device(8, sc.n_solvers, out["pobj"], out["exit"])
     torch.cuda.synchronize()
@@ -101,4 +101,6 @@ def test_shmpc_pipeline_matches_oracle(dev, oracle_mod):
     assert np.array_equal(ex, ref["status"])
     ok = ex == 1
     assert np.abs(out["xtraj"].cpu().numpy()[ok] - ref["xtraj"][ok]).max() <= 1e-4
-    assert np.array_equal(best.cpu().numpy(), select_lowest_cost(ref["pobj"], ref["status"], sc.n_solvers))
+    from conftest import picks_equivalent
+    assert picks_equivalent(best.cpu().numpy(), select_lowest_cost(ref["pobj"], ref["status"], sc.n_solvers),
+                            ref["pobj"])
