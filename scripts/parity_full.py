@@ -62,7 +62,18 @@ def compare(cfg, S, ws, first=0):
     # every accepted step from a converged QP
     path = (bad & (got["info"][:, 0] == ref["sqp_iter"]) & (got["info"][:, 1] == ref["qp_iter"]) &
             (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0))
+    # successful solves whose interior-point path differed (total IPM iterations, or a QP that hit
+    # the iteration cap on one side): on dual-degenerate QPs (C5) rounding decides
+    # the path, and the trajectories then differ by more than rounding
+    path_ok = ok & (got["info"][:, 1] == ref["qp_iter"]) & ((got["info"][:, 3] > 0) == (ref["qp_maxiter"] > 0))
+    over = np.flatnonzero(ok & (dx > 1e-4))
     return {"config": cfg, "qp_warm_start": ws, "solves": int(len(same)), "exit_agreement": float(same.mean()),
+            "max_abs_dx_success_same_path": float(dx[path_ok].max()) if path_ok.any() else None,
+            "success_solves_other_path": int((ok & ~path_ok).sum()),
+            "success_dx_over_1e-4": [{"i": int(i), "dx": float(dx[i]), "gpu_info": got["info"][i].tolist(),
+                                      "oracle_qp_iter": int(ref["qp_iter"][i]),
+                                      "oracle_qp_maxiter": int(ref["qp_maxiter"][i]),
+                                      "same_path": bool(path_ok[i])} for i in over[:20]],
             "success_frac": float((ref["status"] == 1).mean()), "rti_iters_per_solve": float(ref["sqp_iter"].mean()),
             "qp_iters_per_solve_gpu": float(got["info"][:, 1].mean()), "qp_iters_per_solve_oracle": float(ref["qp_iter"].mean()),
             "max_abs_dx_success": float(dx[ok].max()) if ok.any() else None,
