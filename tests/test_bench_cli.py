@@ -15,6 +15,16 @@ def test_gpus_flag_must_match_world_size():
     assert "WORLD_SIZE=1" in r.stderr and "torch.distributed.run" in r.stderr
 
 
+def test_unknown_collective_backend_is_refused():
+    """MPCG_BENCH_BACKEND selects RCCL (default) or the gloo rehearsal; anything else stops
+    before any GPU call."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MPCG_BENCH_BACKEND"] = "mpi"
+    r = subprocess.run([sys.executable, "bench.py"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "MPCG_BENCH_BACKEND=mpi" in r.stderr
+
+
 def test_source_hash_tracks_kernel_sources():
     sys.path.insert(0, ROOT)
     from oscar_mpc_planner_mr_modification_amd import _build
