@@ -17,7 +17,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
 
-DEFAULT_SCENES = {"C2": 1024, "C4": 2048, "C5": 2048, "C3": 4096, "C1": 1024}
+DEFAULT_SCENES = {"C2": 1024, "C4": 2048, "C5": 2048, "C3": 4096, "C1": 1024, "JS": 4096}
+GUESSES = {"JS": 5}   # the bench's guesses per scene (DEFAULT_GUESSES in bench.py); others 8
 
 
 def inputs(cfg, S, first=0):
@@ -31,7 +32,7 @@ def inputs(cfg, S, first=0):
         b = make_c3_batch(lay, S, first_scene=first)
     else:
         from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
-        b = make_batch(lay, S, 8 if cfg != "C1" else 1, first_scene=first, workers=16)
+        b = make_batch(lay, S, GUESSES.get(cfg, 8), first_scene=first, workers=16)
     return lay, b
 
 
