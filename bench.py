@@ -17,6 +17,10 @@ Scene data is uploaded once before the timed region (inputs resident in HBM).
     python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N > 1` without a launcher (no WORLD_SIZE in the environment) starts the N
+rank processes itself: torch.distributed.run as a CHILD process (one rank per GPU,
+RCCL), before this process touches torch or the GPU, and exits with its code.
+
 Rank 0 prints one JSON line.  `roofline` prices the solve kernel against the
 fp64 vector peak with the algorithm's analytic operation count
 (oscar_mpc_planner_mr_modification_amd/flopmodel.py, times the SQP and IPM
@@ -88,6 +92,67 @@ def load_counters(path, config, batch):
     return tj.get("hbm_bytes_per_launch"), f64, f"profiles/{tj.get('tag')}"
 
 
+def cpu_share():
+    """CPUs this job may use on the host: nproc, the affinity mask, the cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us) and OMP_NUM_THREADS if set.
+    On the GPU box nproc counts the whole machine while the job's share is a slice of it
+    (the pool sets OMP_NUM_THREADS to that share), so the CPU baseline's widest leg runs
+    on `share` threads and reports nproc beside it."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    share = aff if quota is None else max(1, min(aff, int(quota)))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        share = min(share, omp)
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "omp_num_threads": omp or None,
+            "share": share}
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: run torch.distributed.run as a child process
+    (one rank per GPU, rendezvous on 127.0.0.1, a free port) and return its exit code.  The
+    parent has not imported torch nor touched the GPU; it never re-execs itself."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def spawn_check(world):
+    """--spawn-check (CPU test of the rank spawning): every rank joins a gloo group and counts
+    the ranks; rank 0 prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"spawn_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
+                          "local_ranks": world}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------- workloads
 class Workload:
     """One config's GPU step: `step(timed)` enqueues one control step of every scene
@@ -97,7 +162,7 @@ class Workload:
     def __init__(self, args, lay, rank, world, dev):
         self.args, self.lay, self.rank, self.world, self.dev = args, lay, rank, world, dev
         self.S = args.scenes or DEFAULT_SCENES[args.config]
-        self.threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        self.threads = cpu_share()["share"]
 
     def host_inputs(self, lo, hi):
         """host copies (params, warm, xinit) of solves [lo, hi) for the oracle check"""
@@ -363,18 +428,28 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle (CPU baseline and parity)")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default profiles/traffic_<config>.json)")
+    ap.add_argument("--spawn-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.guesses is None:
         args.guesses = DEFAULT_GUESSES.get(args.config, 8)
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
 
-    # one process per GPU: --gpus must match the launcher's world size (checked before any GPU call)
+    # one process per GPU.  Without a launcher, --gpus N > 1 starts the N ranks as a child
+    # torch.distributed.run (before any torch / GPU call here); under a launcher --gpus must
+    # match its world size (checked before any GPU call)
+    backend = os.environ.get("MPCG_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        sys.exit(f"bench.py: MPCG_BENCH_BACKEND={backend}: expected nccl or gloo")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world:
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as `python -m "
-                 f"torch.distributed.run --nnodes=1 --nproc-per-node {args.gpus} --master-addr 127.0.0.1 "
-                 f"bench.py --gpus {args.gpus} ...` (one rank per GPU)")
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE={world} (one rank per GPU: "
+                 f"`python -m torch.distributed.run --nnodes=1 --nproc-per-node {args.gpus} --master-addr "
+                 f"127.0.0.1 bench.py --gpus {args.gpus} ...`, or plain `bench.py --gpus {args.gpus}`)")
+    if args.spawn_check:
+        return spawn_check(world)
 
     import torch
     import torch.distributed as dist
@@ -384,11 +459,12 @@ def main():
     # RCCL (one rank per GPU) is the product path; MPCG_BENCH_BACKEND=gloo is a rehearsal of the
     # multi-rank code on fewer GPUs (ranks share devices round-robin, collectives staged through
     # the host) and is labelled as such in the line
-    backend = os.environ.get("MPCG_BENCH_BACKEND", "nccl")
-    if backend not in ("nccl", "gloo"):
-        sys.exit(f"bench.py: MPCG_BENCH_BACKEND={backend}: expected nccl or gloo")
+    n_dev = torch.cuda.device_count()  # (does not initialise the GPU)
     if backend == "gloo":
-        local_rank = local_rank % max(1, torch.cuda.device_count())
+        local_rank = local_rank % max(1, n_dev)
+    elif world > n_dev:
+        sys.exit(f"bench.py: --gpus {world} with RCCL needs {world} GPUs, {n_dev} visible "
+                 "(MPCG_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
@@ -431,6 +507,11 @@ def main():
         elapsed = float(te[0])
         phase_ms = {p: float(te[1 + j]) for j, p in enumerate(wl.phases)}
     kern_ms = phase_ms["solve"]
+    ranks_seen = 1
+    if world > 1:
+        rs = torch.ones(1, dtype=torch.float64, device=dev)
+        all_reduce_(rs, dist.ReduceOp.SUM)
+        ranks_seen = int(rs.item())
     B = wl.B
     value = args.steps * B * world / elapsed
     exit_h, xt_h, info_h = (wl.out[k].cpu().numpy() for k in ("exit", "xtraj", "info"))
@@ -475,8 +556,10 @@ def main():
     if isinstance(wl, TmpcWorkload):
         stats["scene_feasible_frac"] = float(ok.reshape(-1, wl.G).any(1).mean())
     result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
-        "ranks_seen": dist.get_world_size() if world > 1 else 1,
+        "metric": METRIC, "value": round(value, 2), "unit": "solves/s",
+        # distinct devices used (a gloo rehearsal shares them between ranks)
+        "n_gpus": world if backend == "nccl" else min(world, n_dev),
+        "ranks_seen": ranks_seen,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": f"synthetic (seeded scenes, SURVEY.md §8d {args.config})",
@@ -490,6 +573,10 @@ def main():
         "solver_stats": stats,
         "phases_ms": {p: round(v, 4) for p, v in phase_ms.items()},
     }
+    if backend == "gloo" and world > 1:
+        # several ranks on one device: the rate is not a scaling figure
+        result["rehearsal"] = {"backend": "gloo", "ranks": world, "devices": min(world, n_dev),
+                               "rate_is_scaling_figure": False}
 
     if not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -514,12 +601,17 @@ def main():
                 orc.solve_batch(prm, wrm, xin, nthreads=nthreads)
                 return len(prm) / (time.perf_counter() - tc)
 
+            share = cpu_share()
             result["cpu_baseline"] = {"value": round(done / t_cpu, 2), "unit": "solves/s", "cores": threads,
                                       "kind": "port",
                                       "sample": f"first {done} of the {B} solves of this batch, C oracle (same "
-                                                f"algorithm), OpenMP {threads} threads",
+                                                f"algorithm), OpenMP {threads} threads = the job's CPU share",
                                       "single_thread_solves_per_s": round(rate(64, 1), 2),
-                                      "eight_thread_solves_per_s": round(rate(512, 8), 2) if threads >= 8 else None}
+                                      "eight_thread_solves_per_s": round(rate(512, 8), 2) if threads >= 8 else None,
+                                      "host": share,
+                                      "nproc_leg": ("same as value (share == nproc)" if share["share"] == share["nproc"]
+                                                    else f"value is the {share['share']}-thread share of this job; "
+                                                         f"nproc = {share['nproc']} counts the whole host")}
             result["vs_cpu_baseline"] = round(value / (done / t_cpu), 2)
             ranks_checked = 1
         else:

@@ -37,10 +37,17 @@ extern "C" {
 #define MPCG_NU 2            /* the unicycle models */
 #define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 5
+#define MPCG_ABI_VERSION 6
 /* mpcg_problem.model */
 #define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
 #define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
+/* mpcg_problem.nlp_solver: solver_settings.acados.solver_type (settings.yaml:19,
+ * generate_acados_solver.py:153) */
+#define MPCG_NLP_SQP_RTI 0         /* sqp_iters SQP-RTI iterations per solve (the reference's loop of
+                                      Solver_acados_solve calls, acados_solver_interface.cpp:86-119) */
+#define MPCG_NLP_SQP 1             /* one full acados SQP call (the reference sets _num_iterations = 1,
+                                      :27-29): up to nlp_max_iter iterations, converged when the four NLP
+                                      residuals are below nlp_tol */
 
 /* Problem description: the generated solver's dimensions + the parameter
  * map (parameter_map.yaml written by solver_generator/generate_solver.py:34-46)
@@ -76,11 +83,20 @@ typedef struct mpcg_problem {
     int i_w_tangle, i_w_tcont;     /* terminal_angle / terminal_contouring: read by the bicycle model's
                                       CurvatureAwareContouring at stage N-1 (curvature_aware_contouring.py:94-103,
                                       Forces' per-stage objective, generate_forces_solver.py:50-59) */
-    int qp_warm_start;             /* qp_solver_warm_start (generate_acados_solver.py:173): 2 = HPIPM primal +
-                                      dual warm start of every QP from the previous QP's solution (the capsule's
-                                      QP memory), slacks and multipliers clipped below at qp_ws_thr; the first
-                                      QP of a call starts warm only from mpcg_io.qp_in.  0 = cold start */
+    int qp_warm_start;             /* qp_solver_warm_start (generate_acados_solver.py:173, default 2): 2 = HPIPM
+                                      primal + dual warm start from the previous QP's solution (the capsule's QP
+                                      memory), slacks and multipliers clipped below at qp_ws_thr; 0 = cold start.
+                                      Applies to every QP of an acados call after its first, and to the first
+                                      one only with qp_warm_first (so every SQP-RTI QP starts cold by default) */
     double qp_ws_thr;              /* 0.1 */
+    /* ABI 6 */
+    int nlp_solver;                /* MPCG_NLP_SQP_RTI (default) or MPCG_NLP_SQP */
+    int nlp_max_iter;              /* MPCG_NLP_SQP: acados nlp_solver_max_iter (acados_template default 100; the
+                                      reference leaves it unset, generate_acados_solver.py:154) */
+    double nlp_tol;                /* MPCG_NLP_SQP: solver_options.tol 1e-2 (generate_acados_solver.py:144) on the
+                                      stationarity, dynamics, inequality and complementarity residuals */
+    int qp_warm_first;             /* acados warm_start_first_qp (default 0): the first QP of a call also starts
+                                      warm (from mpcg_io.qp_in, or in SQP-RTI from the previous iteration's QP) */
 } mpcg_problem;
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,
@@ -160,8 +176,14 @@ typedef struct mpcg_io {
 } mpcg_io;
 
 /* Batched solve on device buffers, enqueued on `stream` (hipStream_t, NULL =
- * default stream).  Returns 0 on a successful launch. */
+ * default stream).  Returns 0 on a successful launch.  Instances whose stage blocks live
+ * in global memory (N 30 with 12 obstacles, the bicycle) use a device workspace that
+ * libmpcg keeps per stream on the stream's device (reused by later calls on the stream,
+ * released by mpcg_release_stream_workspace); contexts own theirs. */
 int mpcg_solve(const mpcg_problem *pr, int batch, const mpcg_io *io, void *stream);
+
+/* Frees the workspace mpcg_solve keeps for `stream` (after the stream's work).  Returns 0. */
+int mpcg_release_stream_workspace(void *stream);
 
 /* A persistent solve context: device buffers and pinned staging for up to
  * `max_batch` solves plus a private stream, so that one Solver::solve()

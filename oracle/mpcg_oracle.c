@@ -493,6 +493,18 @@ void orc_mirror(int n, double *H, double eps) {
         }
 }
 
+/* ORC_KFORM (a second build, test infrastructure for rounding-sensitivity records only:
+ * scripts/rounding_proxy.py): the SAME algorithm with the GPU kernel's arithmetic forms
+ * -- reciprocal square roots and reciprocal multiplies instead of sqrt and divisions
+ * (the 2x2 Cholesky through 1/sqrt(m00) and 1/sqrt(det)), the kernel's operand order in
+ * the row residuals and Newton terms -- compiled with FMA contraction.  Not the oracle:
+ * the default build is the literal restatement. */
+#ifdef ORC_KFORM
+#define KF 1
+#else
+#define KF 0
+#endif
+
 /* ------------------------------------------------------------------ */
 /* OCP-QP: Riccati-based Mehrotra primal-dual interior point            */
 /* (PARTIAL_CONDENSING_HPIPM with cond_N = N, qp_tol 1e-5, iter_max 50:  */
@@ -509,6 +521,7 @@ typedef struct {
     int *hsgn;
     /* Riccati storage */
     double L[NU][NU], Y[NU][NX], P[NX][NX], p[NX], y[NU];
+    double il[NU];  /* ORC_KFORM: reciprocal pivots 1/L_ii */
     double Hh[NZ][NZ], q[NZ];
     double dz[NZ], ddz[NZ], pi[NX], pin[NX];
 } qp_stage;
@@ -543,8 +556,16 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
             for (int i = 0; i < NX; i++) r[NU + i] -= w->st[k - 1].pi[i];
         for (int c = 0; c < S->ni; c++) {
             for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * S->lam[c];
-            double acc = S->t[c] - S->d[c];
-            for (int i = 0; i < NZ; i++) acc += S->D[c][i] * S->dz[i];
+            double acc;
+            if (KF) {
+                /* kernel: rin = D.dz + t - gap */
+                double dd = 0.0;
+                for (int i = 0; i < NZ; i++) dd += S->D[c][i] * S->dz[i];
+                acc = dd + S->t[c] - S->d[c];
+            } else {
+                acc = S->t[c] - S->d[c];
+                for (int i = 0; i < NZ; i++) acc += S->D[c][i] * S->dz[i];
+            }
             S->rin[c] = acc;
             if (fabs(acc) > i_max) i_max = fabs(acc);
             comp += S->lam[c] * S->t[c];
@@ -602,6 +623,27 @@ static int riccati_factor(qp_ws *w) {
                 for (int m = 0; m < NX; m++) acc += F[m][i] * PF[m][j];
                 M[i][j] = acc;
             }
+        if (KF && NU == 2) {
+            /* kernel: both reciprocal square roots from the block entries,
+             * 1/l11 = l00 / sqrt(m00 m11 - m10^2) */
+            const double m00 = M[0][0], m10 = M[1][0], m11 = M[1][1];
+            if (!(m00 > 0.0)) return -1;
+            const double il00 = 1.0 / sqrt(m00);
+            const double det = fma(m00, m11, -(m10 * m10));
+            if (!(det > 0.0)) return -1;
+            const double ild = 1.0 / sqrt(det);
+            S->L[0][0] = m00 * il00; S->L[1][0] = m10 * il00; S->L[0][1] = 0.0;
+            S->il[0] = il00; S->il[1] = S->L[0][0] * ild;
+            S->L[1][1] = 1.0 / S->il[1];
+            for (int j = 0; j < NX; j++) {
+                S->Y[0][j] = M[0][NU + j] * S->il[0];
+                S->Y[1][j] = (M[1][NU + j] - S->L[1][0] * S->Y[0][j]) * S->il[1];
+            }
+            for (int i = 0; i < NX; i++)
+                for (int j = 0; j < NX; j++)
+                    S->P[i][j] = M[NU + i][NU + j] - S->Y[0][i] * S->Y[0][j] - S->Y[1][i] * S->Y[1][j];
+            continue;
+        }
         /* Cholesky of Muu (L L' = Muu) */
         for (int j = 0; j < NU; j++) {
             double d = M[j][j];
@@ -658,7 +700,7 @@ static void riccati_solve(qp_ws *w) {
         for (int i = 0; i < NU; i++) { /* y = L^{-1} m_u */
             double acc = m[i];
             for (int q = 0; q < i; q++) acc -= S->L[i][q] * S->y[q];
-            S->y[i] = acc / S->L[i][i];
+            S->y[i] = (KF && NU == 2) ? acc * S->il[i] : acc / S->L[i][i];
         }
         for (int i = 0; i < NX; i++) {
             double acc = m[NU + i];
@@ -679,7 +721,7 @@ static void riccati_solve(qp_ws *w) {
         for (int i = NU - 1; i >= 0; i--) { /* L' du = -c */
             double acc = -c[i];
             for (int q = i + 1; q < NU; q++) acc -= S->L[q][i] * du[q];
-            du[i] = acc / S->L[i][i];
+            du[i] = (KF && NU == 2) ? acc * S->il[i] : acc / S->L[i][i];
         }
         for (int i = 0; i < NU; i++) S->ddz[i] = du[i];
         for (int i = 0; i < NX; i++) S->ddz[NU + i] = (k == 0) ? 0.0 : dx[i];
@@ -711,7 +753,8 @@ static void build_q(qp_ws *w) {
             S->q[i] = acc;
         }
         for (int c = 0; c < S->ni; c++) {
-            double coef = S->lam[c] + (S->lam[c] * S->rin[c] - S->rc[c]) / S->t[c];
+            double coef = KF ? S->lam[c] + (S->lam[c] * S->rin[c] - S->rc[c]) * (1.0 / S->t[c])
+                             : S->lam[c] + (S->lam[c] * S->rin[c] - S->rc[c]) / S->t[c];
             for (int i = 0; i < NZ; i++) S->q[i] += S->D[c][i] * coef;
         }
     }
@@ -725,12 +768,26 @@ static void ineq_steps(qp_ws *w, double *dtv_unused) {
             double acc = 0.0;
             for (int i = 0; i < NZ; i++) acc += S->D[c][i] * S->ddz[i];
             S->dt[c] = -S->rin[c] - acc;
-            S->dl[c] = -(S->rc[c] + S->lam[c] * S->dt[c]) / S->t[c];
+            S->dl[c] = KF ? -(S->rc[c] + S->lam[c] * S->dt[c]) * (1.0 / S->t[c])
+                          : -(S->rc[c] + S->lam[c] * S->dt[c]) / S->t[c];
         }
     }
 }
 
 static double max_step(qp_ws *w) {
+    if (KF) {
+        /* kernel: 1 / max over rows of -dt/t and -dl/l */
+        double rmax = 0.0;
+        for (int k = 0; k <= w->N; k++) {
+            qp_stage *S = &w->st[k];
+            for (int c = 0; c < S->ni; c++) {
+                double a = -S->dt[c] * (1.0 / S->t[c]);
+                if (a > rmax) rmax = a;
+                if (S->dl[c] < 0.0) { a = -S->dl[c] * (1.0 / S->lam[c]); if (a > rmax) rmax = a; }
+            }
+        }
+        return rmax > 0.0 ? 1.0 / rmax : 1e300;
+    }
     double amax = 1e300;
     for (int k = 0; k <= w->N; k++) {
         qp_stage *S = &w->st[k];
@@ -797,7 +854,7 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
             qp_stage *S = &w->st[k];
             memcpy(S->Hh, S->H, sizeof S->H);
             for (int c = 0; c < S->ni; c++) {
-                double wc = S->lam[c] / S->t[c];
+                double wc = KF ? S->lam[c] * (1.0 / S->t[c]) : S->lam[c] / S->t[c];
                 for (int i = 0; i < NZ; i++) {
                     if (S->D[c][i] == 0.0) continue;
                     for (int j = 0; j < NZ; j++) S->Hh[i][j] += S->D[c][i] * wc * S->D[c][j];
@@ -1054,7 +1111,8 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0, n_maxit = 0;
     double res_eq = 0.0;
 
-    for (int it = 0; it < pr->sqp_iters; it++) {
+    const int sqp_mode = pr->nlp_solver == 1;
+    for (int it = 0; sqp_mode || it < pr->sqp_iters; it++) {
         res_eq = linearise(pr, params, z, pi, lamh, lh, uh, &w, hh);
         /* x0 elimination: lbx_0 = ubx_0 = xinit (acados_solver_interface.cpp:124-125) */
         for (int i = 0; i < NX; i++) w.st[0].dz[NU + i] = xinit[i] - z[0][NU + i];
@@ -1069,10 +1127,23 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
                                     : (S->hrow[c] >= 0 ? lamh[(size_t)k * 2 * nh + 2 * S->hrow[c] + S->hsgn[c]] : 0.0);
         }
         nlp_residuals(&w, lrp, &res_stat, &res_ineq, &res_comp);
+        if (sqp_mode) {
+            /* acados SQP termination at this linearisation point */
+            if (res_stat < pr->nlp_tol && res_eq < pr->nlp_tol && res_ineq < pr->nlp_tol && res_comp < pr->nlp_tol) {
+                acados_status = AC_SUCCESS;
+                break;
+            }
+            if (it >= pr->nlp_max_iter) {
+                acados_status = AC_MAXITER;
+                break;
+            }
+        }
 
-        /* ---- feedback phase: QP ---- */
+        /* ---- feedback phase: QP ---- (warm: every QP of an acados call after its first;
+         * the first with warm_start_first_qp) */
         int qit = 0;
-        qp_status = qp_solve(pr, &w, &qit, have_qp && pr->qp_warm_start == 2);
+        const int warm = have_qp && pr->qp_warm_start == 2 && ((sqp_mode && it > 0) || pr->qp_warm_first);
+        qp_status = qp_solve(pr, &w, &qit, warm);
         have_qp = 1;
         qp_iter_total += qit;
         sqp_iter++;
@@ -1092,8 +1163,9 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
         }
         for (int i = 0; i < NU; i++) z[N][i] = 0.0;
         acados_status = AC_SUCCESS;
-        /* acados_solver_interface.cpp:105: break when the QP did not succeed */
-        if (qp_status != AC_SUCCESS) break;
+        /* SQP-RTI, acados_solver_interface.cpp:105: break when the QP did not succeed (a full
+         * SQP call continues after a max-iter QP) */
+        if (!sqp_mode && qp_status != AC_SUCCESS) break;
     }
 
     double pobj = 0.0;

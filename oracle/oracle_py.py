@@ -43,6 +43,7 @@ class OrcProblem(C.Structure):
         ("res_eq_fail", C.c_double),
         ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int), ("nu", C.c_int),
         ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
+        ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
     ]
 
 
@@ -128,10 +129,16 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.qp_mu0 = opts.get("qp_mu0", 1.0)
     pr.qp_thr0 = opts.get("qp_thr0", 1.0)
     pr.res_eq_fail = opts.get("res_eq_fail", 1e-2)
-    # IPM start: cold by default; 2 = the restated HPIPM warm start (qp_solver_warm_start,
-    # generate_acados_solver.py:173) with HPIPM's floor (DESIGN.md §2 "QP start")
-    pr.qp_warm_start = opts.get("qp_warm_start", 0)
+    # QP start as the reference configures it: qp_solver_warm_start 2 (generate_acados_solver.py:173)
+    # with warm_start_first_qp off -- every SQP-RTI QP starts cold; qp_warm_first=1 warm-starts the
+    # first QP of each call too (DESIGN.md §2 "QP start")
+    pr.qp_warm_start = opts.get("qp_warm_start", 2)
     pr.qp_ws_thr = opts.get("qp_ws_thr", 0.1)
+    pr.qp_warm_first = opts.get("qp_warm_first", 0)
+    # solver_type: "SQP_RTI" (default) or "SQP" (one acados SQP call, tol 1e-2, max_iter 100)
+    pr.nlp_solver = {"SQP_RTI": 0, "SQP": 1}[opts.get("solver_type", "SQP_RTI")]
+    pr.nlp_max_iter = opts.get("nlp_max_iter", 100)
+    pr.nlp_tol = opts.get("nlp_tol", 1e-2)
     return pr
 
 

@@ -168,7 +168,10 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
     const mpcg::YamlNode& cfg = SolverConfig::settings();
     dt = cfg["integrator_step"].as<double>();
     _num_iterations = cfg["solver_settings"]["acados"]["iterations"].as<int>();
-    if (cfg["solver_settings"]["acados"]["solver_type"].as<std::string>() == "SQP") _num_iterations = 1;
+    const std::string solver_type = cfg["solver_settings"]["acados"]["solver_type"].as<std::string>();
+    if (solver_type != "SQP" && solver_type != "SQP_RTI")
+        fatal("solver_settings.acados.solver_type must be SQP_RTI or SQP, not '" + solver_type + "'");
+    if (solver_type == "SQP") _num_iterations = 1;
 
     // the kernel's problem description from the generator's maps
     std::vector<std::string> names;
@@ -191,6 +194,9 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
     if (mpcg_problem_from_map_model(&_problem, SOLVER_MODEL, N, (int)nx, npar, (int)names.size(), cnames.data(),
                                     idx.data(), lb.data(), ub.data(), dt, _num_iterations) != 0)
         fatal(std::string("parameter map: ") + mpcg_last_error());
+    // solver_type SQP: each Solver_acados_solve is a full acados SQP call (nlp_solver_type,
+    // generate_acados_solver.py:153; tol 1e-2, :144), run to its own termination by the kernel
+    if (solver_type == "SQP") _problem.nlp_solver = MPCG_NLP_SQP;
     if (mpcg_supported(&_problem) != 0)
         fatal("no compiled kernel instance for N=" + std::to_string(N) + ", nx=" + std::to_string(nx) + " with " +
               std::to_string(_problem.n_lin) + " halfspaces, " + std::to_string(_problem.n_ell) + " obstacles and " +

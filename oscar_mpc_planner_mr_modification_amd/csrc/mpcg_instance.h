@@ -16,32 +16,29 @@
 
 extern "C" {
 /* launcher of one compiled instance: enqueues the solve of `batch` problems on `stream`
- * and returns the hipError_t of the launch */
+ * and returns the hipError_t of the launch.  `workspace`: device memory of at least
+ * batch x the instance's workspace bytes per solve on the stream's device (instances whose
+ * stage blocks do not fit the LDS budget keep them there), or NULL when it needs none */
 typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream,
-                                    unsigned long long* stamps);
-/* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher and the
- * doubles of one solve's QP memory.  Returns 0 (a shape already present keeps its first
- * launcher). */
+                                    unsigned long long* stamps, void* workspace);
+/* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher, the
+ * doubles of one solve's QP memory and the workspace bytes of one solve.  Returns 0 (a
+ * shape already present keeps its first launcher). */
 int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
-                           int qp_mem_size);
-/* libmpcg.so's device workspace of `stream` (instances whose stage blocks do not fit the
- * LDS budget keep them there): at least `bytes`, valid for work enqueued on that stream;
- * NULL on allocation failure. */
-void* mpcg_stream_workspace(void* stream, size_t bytes);
+                           int qp_mem_size, long long workspace_bytes_per_solve);
 }
 
 namespace mpcg {
 
 template <class C>
-int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps) {
+int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps,
+                    void* workspace) {
     // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
-    // the full variant only when the call needs QP memory, the warm start or the residuals
-    double* gws = nullptr;
-    if constexpr (gfh_doubles<C>() > 0) {
-        gws = (double*)mpcg_stream_workspace(stream, (size_t)batch * gfh_doubles<C>() * sizeof(double));
-        if (!gws) return (int)hipErrorOutOfMemory;
-    }
-    if (io->stats || io->qp_in || io->qp_out || pr->qp_warm_start == 2)
+    // the full variant only when the call needs QP memory, the warm start, the residuals or
+    // the full SQP
+    double* gws = (double*)workspace;
+    if (gfh_doubles<C>() > 0 && !gws) return (int)hipErrorInvalidValue;
+    if (io->stats || io->qp_in || io->qp_out || needs_full(*pr))
         hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
                            stamps, gws);
     else
@@ -52,7 +49,8 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
 
 template <class C>
 int register_instance() {
-    return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM);
+    return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM,
+                                  (long long)(gfh_doubles<C>() * sizeof(double)));
 }
 
 }  // namespace mpcg

@@ -87,7 +87,8 @@ static unsigned long long* g_stamps = nullptr;  // diagnostic stamp buffer (MPCG
 struct Inst {
     int model = 0, N = 0, nl = 0, ne = 0, ns = 0, nx = 0;
     mpcg_instance_launch fn = nullptr;
-    int qpm = 0;  // doubles of one solve's QP memory (Cfg::QPM)
+    int qpm = 0;         // doubles of one solve's QP memory (Cfg::QPM)
+    long long ws = 0;    // workspace bytes of one solve (GFH stage blocks; 0: none)
 };
 static std::mutex& registry_mutex() {
     static std::mutex m;
@@ -109,10 +110,9 @@ static Inst find_instance(const mpcg_problem& pr) {
     return {};
 }
 
-using Fn = mpcg_instance_launch;
-
-static int launch(Fn fn, const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream) {
-    const int e = fn(&pr, batch, &io, (void*)stream, g_stamps);
+static int launch(const Inst& in, const mpcg_problem& pr, int batch, const mpcg_io& io, hipStream_t stream,
+                  void* ws) {
+    const int e = in.fn(&pr, batch, &io, (void*)stream, g_stamps, ws);
     if (e != (int)hipSuccess) {
         g_err = std::string("sqp_kernel launch: ") + hipGetErrorString((hipError_t)e);
         return -1;
@@ -120,10 +120,68 @@ static int launch(Fn fn, const mpcg_problem& pr, int batch, const mpcg_io& io, h
     return 0;
 }
 
-static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
+// Workspaces of the raw mpcg_solve path, one per (device, stream) on the STREAM's device:
+// kernels enqueued on one stream run in order, so one buffer serves every call on it.  The
+// lock is held until the launch is enqueued, so a larger request from another thread (which
+// synchronises the stream before it replaces the buffer) cannot free it under a launch.
+struct StreamWs {
+    int dev;
+    void* stream;
+    void* ptr;
+    size_t size;
+};
+static std::mutex g_ws_mutex;
+static std::vector<StreamWs> g_ws;
+
+static int stream_device(hipStream_t stream, int* dev) {
+    if (stream) return hipStreamGetDevice(stream, dev) == hipSuccess ? 0 : -1;
+    return hipGetDevice(dev) == hipSuccess ? 0 : -1;
+}
+
+static int launch_on_stream(const Inst& in, const mpcg_problem& pr, int batch, const mpcg_io& io,
+                            hipStream_t stream) {
+    if (in.ws <= 0) return launch(in, pr, batch, io, stream, nullptr);
+    const size_t bytes = (size_t)batch * (size_t)in.ws;
+    int dev = 0;
+    if (stream_device(stream, &dev)) { g_err = "mpcg_solve: no device for the stream"; return -1; }
+    std::lock_guard<std::mutex> l(g_ws_mutex);
+    StreamWs* w = nullptr;
+    for (StreamWs& e : g_ws)
+        if (e.dev == dev && e.stream == (void*)stream) w = &e;
+    if (!w) {
+        g_ws.push_back(StreamWs{dev, (void*)stream, nullptr, 0});
+        w = &g_ws.back();
+    }
+    if (w->size < bytes) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) cur = dev;
+        bool ok = hipSetDevice(dev) == hipSuccess;
+        if (ok && w->ptr) {
+            ok = hipStreamSynchronize(stream) == hipSuccess;
+            (void)hipFree(w->ptr);
+            w->ptr = nullptr;
+            w->size = 0;
+        }
+        if (ok && hipMalloc(&w->ptr, bytes) != hipSuccess) { w->ptr = nullptr; ok = false; }
+        (void)hipSetDevice(cur);
+        if (!ok) { g_err = "mpcg_solve: workspace allocation failed"; return -1; }
+        w->size = bytes;
+    }
+    return launch(in, pr, batch, io, stream, w->ptr);
+}
+
+static int check_problem(const mpcg_problem* pr, int batch, Inst* inst) {
     if (!pr || batch < 0) { g_err = "invalid arguments"; return -1; }
-    *fn = find_instance(*pr).fn;
-    if (!*fn) {
+    if (pr->nlp_solver != MPCG_NLP_SQP_RTI && pr->nlp_solver != MPCG_NLP_SQP) {
+        g_err = "nlp_solver must be MPCG_NLP_SQP_RTI or MPCG_NLP_SQP";
+        return -1;
+    }
+    if (pr->nlp_solver == MPCG_NLP_SQP && (pr->nlp_max_iter < 0 || !(pr->nlp_tol > 0.0))) {
+        g_err = "MPCG_NLP_SQP needs nlp_max_iter >= 0 and nlp_tol > 0";
+        return -1;
+    }
+    *inst = find_instance(*pr);
+    if (!inst->fn) {
         g_err = "no compiled instance for model=" + std::to_string(pr->model) + " N=" + std::to_string(pr->N) +
                 " nx=" + std::to_string(pr->nx) + " nu=" + std::to_string(pr->nu) +
                 " n_lin=" + std::to_string(pr->n_lin) + " n_ell=" + std::to_string(pr->n_ell) +
@@ -136,7 +194,7 @@ static int check_problem(const mpcg_problem* pr, int batch, Fn* fn) {
 }  // namespace mpcg
 
 extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx,
-                                      mpcg_instance_launch fn, int qp_mem_size) {
+                                      mpcg_instance_launch fn, int qp_mem_size, long long workspace_bytes_per_solve) {
     if (!fn) return -1;
     std::lock_guard<std::mutex> l(mpcg::registry_mutex());
     for (const mpcg::Inst& in : mpcg::registry())
@@ -146,55 +204,19 @@ extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, in
     in.model = model; in.N = N; in.nl = n_lin; in.ne = n_ell; in.ns = n_scen; in.nx = nx;
     in.fn = fn;
     in.qpm = qp_mem_size;
+    in.ws = workspace_bytes_per_solve;
     mpcg::registry().push_back(in);
     return 0;
-}
-
-// Device workspaces per (device, stream) for the instances that keep their stage blocks in
-// global memory (mpcg_instance.h): kernels enqueued on one stream run in order, so one
-// buffer per stream serves them all; a larger request waits for the stream's work before
-// the buffer is replaced.  Kept for the life of the process.
-extern "C" void* mpcg_stream_workspace(void* stream, size_t bytes) {
-    struct Ws {
-        int dev;
-        void* stream;
-        void* ptr;
-        size_t size;
-    };
-    static std::mutex m;
-    static std::vector<Ws> pool;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> l(m);
-    Ws* w = nullptr;
-    for (Ws& e : pool)
-        if (e.dev == dev && e.stream == stream) w = &e;
-    if (!w) {
-        pool.push_back(Ws{dev, stream, nullptr, 0});
-        w = &pool.back();
-    }
-    if (w->size < bytes) {
-        if (w->ptr) {
-            if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return nullptr;
-            (void)hipFree(w->ptr);
-            w->ptr = nullptr;
-            w->size = 0;
-        }
-        if (hipMalloc(&w->ptr, bytes) != hipSuccess) {
-            w->ptr = nullptr;
-            return nullptr;
-        }
-        w->size = bytes;
-    }
-    return w->ptr;
 }
 
 // Persistent context (include/mpcg.h): one device allocation for every
 // buffer of `max_batch` solves, one pinned staging block, a private stream.
 struct mpcg_context {
     mpcg_problem pr;
+    mpcg::Inst inst;
     int max_batch = 0;
     hipStream_t stream = nullptr;
+    void* ws = nullptr;      // the instance's workspace for max_batch solves (on the context's device)
     double* dev = nullptr;   // params | warm | xinit | lam_in | qp_in | xtraj | utraj | pobj | lam_out | qp_out | stats
     double* host = nullptr;  // pinned mirror of the same layout
     int* idev = nullptr;     // exit | info
@@ -323,23 +345,55 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->qp_mu0 = 1.0;
     pr->qp_thr0 = 1.0;
     pr->res_eq_fail = 1e-2;
-    // IPM start: cold (DESIGN.md §2 "QP start" -- the restated HPIPM warm start, qp_warm_start = 2 of
-    // generate_acados_solver.py:173, is available but breaks full-size GPU/oracle parity on C4 / C5)
-    pr->qp_warm_start = 0;
+    // QP start as the reference configures it: qp_solver_warm_start = 2 (generate_acados_solver.py:173)
+    // with acados' warm_start_first_qp off, so the first QP of each acados call starts cold -- every
+    // QP of the SQP-RTI loop (DESIGN.md §2 "QP start"), the first of a full SQP call
+    pr->qp_warm_start = 2;
     pr->qp_ws_thr = 0.1;
+    pr->qp_warm_first = 0;
+    // solver_type SQP_RTI (settings.yaml:19); SQP: tol 1e-2 (generate_acados_solver.py:144) and
+    // acados_template's default nlp_solver_max_iter
+    pr->nlp_solver = MPCG_NLP_SQP_RTI;
+    pr->nlp_max_iter = 100;
+    pr->nlp_tol = 1e-2;
     return 0;
 }
 
-int mpcg_solve(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream) {
-    mpcg::Fn fn;
-    int rc = mpcg::check_problem(pr, batch, &fn);
-    if (rc) return rc;
-    if (batch == 0) return 0;  // nothing to do: buffers may be NULL
+static int check_io(const mpcg_io* io) {
     if (!io || !io->params || !io->warm || !io->xinit || !io->xtraj || !io->utraj || !io->pobj || !io->exit_code) {
         mpcg::g_err = "missing buffer";
         return -1;
     }
-    return mpcg::launch(fn, *pr, batch, *io, (hipStream_t)stream);
+    return 0;
+}
+
+int mpcg_solve(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream) {
+    mpcg::Inst in;
+    int rc = mpcg::check_problem(pr, batch, &in);
+    if (rc) return rc;
+    if (batch == 0) return 0;  // nothing to do: buffers may be NULL
+    if (check_io(io)) return -1;
+    return mpcg::launch_on_stream(in, *pr, batch, *io, (hipStream_t)stream);
+}
+
+int mpcg_release_stream_workspace(void* stream) {
+    std::lock_guard<std::mutex> l(mpcg::g_ws_mutex);
+    for (size_t i = 0; i < mpcg::g_ws.size();) {
+        mpcg::StreamWs& w = mpcg::g_ws[i];
+        if (w.stream == stream) {
+            int cur = 0;
+            if (hipGetDevice(&cur) != hipSuccess) cur = w.dev;
+            if (hipSetDevice(w.dev) == hipSuccess) {
+                (void)hipStreamSynchronize((hipStream_t)stream);
+                if (w.ptr) (void)hipFree(w.ptr);
+            }
+            (void)hipSetDevice(cur);
+            mpcg::g_ws.erase(mpcg::g_ws.begin() + i);
+        } else {
+            ++i;
+        }
+    }
+    return 0;
 }
 
 int mpcg_solve_batch_device(const mpcg_problem* pr, int batch, const double* params, const double* warm,
@@ -350,11 +404,12 @@ int mpcg_solve_batch_device(const mpcg_problem* pr, int batch, const double* par
 }
 
 mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
-    mpcg::Fn fn;
-    if (mpcg::check_problem(pr, max_batch, &fn)) return nullptr;
+    mpcg::Inst in;
+    if (mpcg::check_problem(pr, max_batch, &in)) return nullptr;
     if (max_batch < 1) { mpcg::g_err = "max_batch must be >= 1"; return nullptr; }
     auto* c = new mpcg_context();
     c->pr = *pr;
+    c->inst = in;
     c->max_batch = max_batch;
     const size_t B = max_batch, N = pr->N;
     c->n_par = B * N * pr->npar;
@@ -372,7 +427,8 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
               hipMalloc(&c->dev, c->n_dbl * sizeof(double)) == hipSuccess &&
               hipHostMalloc(&c->host, c->n_dbl * sizeof(double), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->idev, c->n_int * sizeof(int)) == hipSuccess &&
-              hipHostMalloc(&c->ihost, c->n_int * sizeof(int), hipHostMallocDefault) == hipSuccess;
+              hipHostMalloc(&c->ihost, c->n_int * sizeof(int), hipHostMallocDefault) == hipSuccess &&
+              (in.ws <= 0 || hipMalloc(&c->ws, (size_t)max_batch * (size_t)in.ws) == hipSuccess);
     if (!ok) {
         mpcg::g_err = "mpcg_context_create: device allocation failed";
         mpcg_context_destroy(c);
@@ -383,6 +439,8 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
 
 void mpcg_context_destroy(mpcg_context* c) {
     if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ws) (void)hipFree(c->ws);
     if (c->dev) (void)hipFree(c->dev);
     if (c->idev) (void)hipFree(c->idev);
     if (c->host) (void)hipHostFree(c->host);
@@ -392,6 +450,7 @@ void mpcg_context_destroy(mpcg_context* c) {
 }
 
 int mpcg_context_set_iterations(mpcg_context* c, int sqp_iters) {
+    /* (MPCG_NLP_SQP ignores it: one SQP call per solve) */
     if (!c || sqp_iters < 1) { mpcg::g_err = "invalid arguments"; return -1; }
     c->pr.sqp_iters = sqp_iters;
     return 0;
@@ -447,7 +506,7 @@ int mpcg_context_solve(mpcg_context* c, int batch, const mpcg_io* io) {
     mpcg_io dio{d, d + s_par, d + s_par + s_warm, d_lam, d_out, d_out + s_xt, d_out + s_xt + s_ut, c->idev,
                 c->idev + B, d_lo, d_qpi, d_qo, d_st};
     bool ok = hipMemcpyAsync(d, h, n_in * sizeof(double), hipMemcpyHostToDevice, c->stream) == hipSuccess;
-    int rc = ok ? mpcg_solve(&pr, batch, &dio, c->stream) : -5;
+    int rc = ok ? mpcg::launch(c->inst, pr, batch, dio, c->stream, c->ws) : -5;
     if (rc == 0)
         ok = hipMemcpyAsync(h_out, d_out, n_out * sizeof(double), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
              hipMemcpyAsync(c->ihost, c->idev, B * (1 + MPCG_INFO_STRIDE) * sizeof(int), hipMemcpyDeviceToHost,

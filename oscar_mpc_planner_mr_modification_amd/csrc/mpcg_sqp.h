@@ -94,7 +94,11 @@ struct Cfg {
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 12
 #endif
+#ifdef MPCG_STORE_IT_ANY
+    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
+#else
     static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX && PARTS == 3;
+#endif
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     // Linear rows (topology and scenario halfspaces) read their coefficients from the
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
@@ -458,6 +462,13 @@ __device__ __forceinline__ void h_rows(const mpcg_problem& pr, const double* __r
     }
 }
 
+// The FULL variant is needed for a full SQP call (its termination test reads the NLP
+// residuals) and for a first QP that starts warm; the SQP-RTI default (every QP the first
+// of its acados call, cold) runs the lean one.
+__host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
+    return pr.nlp_solver == MPCG_NLP_SQP || (pr.qp_warm_start == 2 && pr.qp_warm_first);
+}
+
 // FULL: the variant with the capsule's QP memory (mpcg_io.qp_in / qp_out), the HPIPM warm
 // start (pr.qp_warm_start == 2) and the NLP residuals of every linearisation
 // (mpcg_io.stats; the drop-in's AcadosInfo).  The lean variant (FULL = false: cold
@@ -620,6 +631,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // start (qp_solver_warm_start 2), the initial point of the first QP; the later QPs
     // start from their predecessor's solution
     const bool qp_warm = FULL && pr.qp_warm_start == 2;
+    // solver_type SQP: one acados SQP call (acados_solver_interface.cpp:27-29), terminated by the
+    // NLP residuals (FULL only)
+    const bool sqp_mode = FULL && pr.nlp_solver == MPCG_NLP_SQP;
     bool have_qp = false;
     if (FULL && io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
         const double* q = io.qp_in + (size_t)sol * C::QPM;
@@ -640,7 +654,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     double res_eq = 0.0;
     double nlp_stat = 0.0, nlp_ineq = 0.0, nlp_comp = 0.0;  // NLP residuals of the last linearisation
 
-    for (int it = 0; it < pr.sqp_iters; ++it) {
+    for (int it = 0; sqp_mode || it < pr.sqp_iters; ++it) {
         // parameter loads are re-issued where they are used rather than hoisted out of
         // the SQP / QP loops into registers that stay live (and spill) across them
         if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
@@ -785,7 +799,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
         // =============== feedback: QP by Riccati interior point ===============
         STAMP_BEGIN();
-        if (FULL && io.stats) {
+        if (FULL && (io.stats || sqp_mode)) {
             // NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
             // multipliers the NLP holds: pi_nlp and, per row, the previous QP's multiplier
             // (FIXED_STEP: lam = lam_qp) or, before any QP, the carried h-row ones (box 0)
@@ -858,7 +872,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             nlp_comp = wave_max(vcp);
             wave_sync();
         }
-        if (qp_warm && have_qp) {
+        if (sqp_mode) {
+            // acados SQP: converged at this linearisation point, or out of iterations (its
+            // residuals and res_eq are the final iterate's either way)
+            if (nlp_stat < pr.nlp_tol && res_eq < pr.nlp_tol && nlp_ineq < pr.nlp_tol && nlp_comp < pr.nlp_tol) {
+                acados_status = AC_SUCCESS;
+                break;
+            }
+            if (it >= pr.nlp_max_iter) {
+                acados_status = AC_MAXITER;
+                break;
+            }
+        }
+        // HPIPM warm start for every QP of an acados call after its first (SQP: it > 0), and for
+        // the first with warm_start_first_qp; SQP-RTI calls consist of one QP each
+        const bool warm_now = qp_warm && have_qp && ((sqp_mode && it > 0) || pr.qp_warm_first);
+        if (warm_now) {
             // HPIPM warm_start 2 (d_ocp_qp_ipm init_var): the previous QP's solution is the
             // initial point -- step and dynamics multipliers stay in LDS, the rows' slacks and
             // multipliers in registers -- with slacks and multipliers clipped below at thr0
@@ -1021,6 +1050,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             ri = wave_max(ri);
             comp = wave_sum(comp);
             const double mu = comp / C::M_TOTAL;
+#ifdef MPCG_TRACE
+            // diagnostic build only (scripts/trace_solve.py): the oracle's ORC_DEBUG line of solve MPCG_TRACE
+            if (sol == MPCG_TRACE && lane == 0)
+                printf("  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", qit, rs, re, ri, mu);
+#endif
             if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { qstat = AC_NAN; break; }
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
@@ -2044,7 +2078,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (LR.h_on(r)) R.nlam[r] = R.l[HB + r];
         wave_sync();
         acados_status = AC_SUCCESS;
-        if (qstat != AC_SUCCESS) break;
+        // SQP-RTI: the reference's loop stops after a QP that did not succeed
+        // (acados_solver_interface.cpp:105); a full SQP call continues after a max-iter QP
+        if (!sqp_mode && qstat != AC_SUCCESS) break;
     }
 
     // ---- completeOneIteration (acados_solver_interface.cpp:162-204)

@@ -37,14 +37,19 @@ class MpcgProblem(C.Structure):
         ("res_eq_fail", C.c_double),
         ("nu", C.c_int), ("model", C.c_int), ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int),
         ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
+        # ABI 6
+        ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
     ]
 
 
 # acados options restated (generate_acados_solver.py:88-173: qp_tol, qp_solver_iter_max, MIRROR
-# epsilon) + the IPM's cold start; qp_warm_start=2 selects the restated HPIPM warm start
-# (qp_solver_warm_start, :173) with HPIPM's floor qp_ws_thr (DESIGN.md §2 "QP start")
+# epsilon, tol) + the IPM's cold start; qp_warm_start=2 (the reference's qp_solver_warm_start, :173)
+# with acados' warm_start_first_qp off (qp_warm_first=0) starts every SQP-RTI QP cold and the
+# later QPs of a full SQP call (solver_type="SQP") warm (DESIGN.md §2 "QP start")
 DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2,
-                       qp_warm_start=0, qp_ws_thr=0.1)
+                       qp_warm_start=2, qp_ws_thr=0.1, qp_warm_first=0, solver_type="SQP_RTI", nlp_max_iter=100,
+                       nlp_tol=1e-2)
+NLP_SOLVER = {"SQP_RTI": 0, "SQP": 1}
 # ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
 UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
 UNICYCLE_UB = (2.0, 0.8, 2000.0, 2000.0, 4 * np.pi, 3.0, 10000.0)
@@ -78,6 +83,10 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.res_eq_fail = o["res_eq_fail"]
     pr.qp_warm_start = o["qp_warm_start"]
     pr.qp_ws_thr = o["qp_ws_thr"]
+    pr.qp_warm_first = o["qp_warm_first"]
+    pr.nlp_solver = NLP_SOLVER[o["solver_type"]]
+    pr.nlp_max_iter = o["nlp_max_iter"]
+    pr.nlp_tol = o["nlp_tol"]
     return pr
 
 
@@ -114,10 +123,10 @@ class MpcgScenarioIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size", "mpcg_qp_mem_size",
            "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
-           "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device")
+           "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device", "mpcg_release_stream_workspace")
 
 

@@ -231,8 +231,9 @@ def prepare_scenario_host(layout: Layout, sc: ScenarioScenes, radius: float = RO
 
 
 def make_shmpc_batch(layout: Layout, n_scenes: int, n_solvers: int = PARALLEL_SOLVERS, n_obs: int = 12,
-                     n_samples: int = 100, seed: int = SEED0, first_scene: int = 0) -> ScenarioBatch:
-    sc = make_shmpc_scenes(layout, n_scenes, n_solvers, n_obs, n_samples, seed, first_scene)
+                     n_samples: int = 100, seed: int = SEED0, first_scene: int = 0,
+                     previous_plan_warm: bool = True) -> ScenarioBatch:
+    sc = make_shmpc_scenes(layout, n_scenes, n_solvers, n_obs, n_samples, seed, first_scene, previous_plan_warm)
     return prepare_scenario_host(layout, sc)
 
 

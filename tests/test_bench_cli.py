@@ -1,5 +1,7 @@
-"""bench.py's launch contract, checked without a GPU: --gpus must match the
-launcher's world size, and the mismatch is reported before any GPU call."""
+"""bench.py's launch contract, checked without a GPU: `bench.py --gpus N` starts its own
+N ranks (a child torch.distributed.run) when no launcher is present, --gpus must match a
+launcher's world size, and both are decided before any GPU call."""
+import json
 import os
 import subprocess
 import sys
@@ -7,12 +9,34 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_gpus_flag_must_match_world_size():
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+def test_gpus_flag_spawns_its_own_ranks():
+    """plain `bench.py --gpus 2` (no launcher) runs two ranks that rendezvous on 127.0.0.1;
+    rank 0 alone prints, and it saw both ranks (--spawn-check: the rank plumbing on gloo)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--spawn-check"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["ranks_seen"] == 2 and line["n_gpus"] == 2
+
+
+def test_gpus_flag_must_match_launcher_world_size():
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK")}
+    env["WORLD_SIZE"] = "1"
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr and "torch.distributed.run" in r.stderr
+
+
+def test_cpu_share_is_bounded_by_the_host():
+    sys.path.insert(0, ROOT)
+    import bench
+    s = bench.cpu_share()
+    assert 1 <= s["share"] <= s["affinity"] <= s["nproc"]
 
 
 def test_unknown_collective_backend_is_refused():

@@ -120,9 +120,24 @@ def test_parity_c3_bicycle(native, torch_dev, oracle_mod, N, n_dec, n_scenes, se
 
 
 def test_single_rti_iteration(native, torch_dev, oracle_mod):
-    """one SQP-RTI iteration == solver_type SQP path (acados_solver_interface.cpp:28-29)"""
+    """one SQP-RTI iteration (one Solver::solveOneIteration, acados_solver_interface.cpp:145-160)"""
     lay, b, ref, got = _run(native, torch_dev, oracle_mod, "C2", 4, 8, 99, sqp_iters=1)
     _compare(ref, got, "C2 sqp_iters=1", require_success=False)
+
+
+@pytest.mark.parametrize("cfg,n_scenes,G,seed", [("C2", 8, 8, 4711), ("C1", 8, 5, 99)])
+def test_parity_full_sqp(native, torch_dev, oracle_mod, cfg, n_scenes, G, seed):
+    """solver_type SQP (settings.yaml:19): the reference sets _num_iterations = 1
+    (acados_solver_interface.cpp:27-29), so one Solver_acados_solve runs acados' full SQP to
+    its own termination -- NLP residuals below tol 1e-2 (generate_acados_solver.py:144) or
+    nlp_solver_max_iter -- with every QP after the first warm-started (qp_solver_warm_start 2,
+    :173; warm_start_first_qp off).  Exit 2 is acados' max-iter status."""
+    lay, b, ref, got = _run(native, torch_dev, oracle_mod, cfg, n_scenes, G, seed, solver_type="SQP")
+    print(f"{cfg} SQP: sqp iterations gpu {got['info'][:, 0].mean():.1f} oracle {ref['sqp_iter'].mean():.1f}, "
+          f"exit codes {np.unique(ref['status'], return_counts=True)}")
+    assert np.array_equal(got["info"][:, 0], ref["sqp_iter"])
+    assert (ref["sqp_iter"] > 1).any()
+    _compare(ref, got, f"{cfg} solver_type SQP")
 
 
 def test_host_path_matches_device(native, torch_dev, oracle_mod):
