@@ -59,8 +59,9 @@ sys.path.insert(0, ROOT)
 METRIC = "SQP solves/s (N=20, 8 obs, 8 guesses) at 1/2/4/8 MI355X; max |x−x_ref|"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (vendor spec)
-DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048, "JS": 4096}
-DEFAULT_GUESSES = {"JS": 5}    # jackalsimulator as shipped: n_paths 4 + the non-guided planner
+DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048, "JS": 4096, "JD": 4096}
+# jackalsimulator / jackal / dingo as shipped: n_paths 4 + the non-guided planner
+DEFAULT_GUESSES = {"JS": 5, "JD": 5}
 CHECK_CHUNK = 256              # solves per oracle call in the check leg
 RANK_SAMPLE = 256              # solves each rank checks at N > 1
 
@@ -193,7 +194,7 @@ class TmpcWorkload(Workload):
         self.gen_s = time.time() - t0
         self.scenes = self.batch.scenes
         self.dsc = native.scenes_to_device(self.scenes, dev)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
         B = self.B
         f64 = dict(dtype=torch.float64, device=dev)
         self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, 7), **f64),
@@ -259,7 +260,7 @@ class C3Workload(Workload):
         self.gen_s = time.time() - t0
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_par, self.d_warm, self.d_xi = t(self.b.params), t(self.b.warm), t(self.b.xinit)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
         f64 = dict(dtype=torch.float64, device=dev)
         self.out = dict(xtraj=torch.empty((S, N + 1, nx), **f64), utraj=torch.empty((S, N, nu), **f64),
                         pobj=torch.empty((S,), **f64), exit=torch.empty((S,), dtype=torch.int32, device=dev),
@@ -328,7 +329,7 @@ class ShmpcWorkload(Workload):
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_sp, self.d_st, self.d_smp = t(self.scenes.stage_params), t(self.scenes.state), t(self.scenes.samples)
         self.d_mw = t(self.scenes.main_warm)   # the main solver's previous plan (scenario.previous_plan)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
         B = self.B
         f64 = dict(dtype=torch.float64, device=dev)
         self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, lay.nvar), **f64),
@@ -423,8 +424,11 @@ def main():
     ap.add_argument("--config", default="C2", choices=sorted(DEFAULT_SCENES))
     ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (C2: 1024, C3: 4096, C4: 2048, C5: 2048)")
     ap.add_argument("--guesses", type=int, default=None, help="planners per scene (8; JS: 5)")
-    ap.add_argument("--qp-warm-start", type=int, default=0, choices=(0, 2),
-                    help="IPM start: 0 cold (default), 2 the restated HPIPM warm start (DESIGN.md §2)")
+    ap.add_argument("--qp-warm-start", type=int, default=2, choices=(0, 2),
+                    help="qp_solver_warm_start: 2 (the reference's, generate_acados_solver.py:173) or 0 cold")
+    ap.add_argument("--qp-warm-first", type=int, default=0, choices=(0, 1),
+                    help="acados warm_start_first_qp: 0 (default: every SQP-RTI QP starts cold), 1 warm-start "
+                         "the first QP of each call too (DESIGN.md §2 'QP start')")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle (CPU baseline and parity)")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default profiles/traffic_<config>.json)")
@@ -550,6 +554,7 @@ def main():
     ok = exit_h == 1
     stats = {"success_frac": float(ok.mean()), "rti_iters_per_solve": float(info_h[:, 0].mean()),
              "qp_iters_per_solve": float(info_h[:, 1].mean()), "qp_warm_start": args.qp_warm_start,
+             "qp_warm_first": args.qp_warm_first,
              "scene_gen_s": round(wl.gen_s, 2)}
     if isinstance(wl, ShmpcWorkload):
         stats["scene_feasible_frac"] = float((wl.best.cpu().numpy() >= 0).mean())
@@ -583,7 +588,7 @@ def main():
         import oracle_py
 
         oracle_py.build()
-        orc = oracle_py.Oracle(lay, qp_warm_start=args.qp_warm_start)
+        orc = oracle_py.Oracle(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
         threads = wl.threads
         if world == 1:
             # CPU baseline: chunks of the same batch until ~cpu_seconds of CPU work, checked on the way

@@ -305,6 +305,11 @@ int mpcg_advance(const mpcg_problem *pr, int n_scenes, int n_guesses, const mpcg
 /* 0 if (model, N, nx, n_lin, n_ell, n_scen) has a compiled kernel instance, else -1 */
 int mpcg_supported(const mpcg_problem *pr);
 
+/* The compiled instance's storage choices as "key=value ..." text (lane parts per stage,
+ * row slots, stored 1/t, LEAN / GFH storage, constant [B A] rows, paired chains, LDS
+ * bytes) into buf[len]: 0, or -1 without an instance. */
+int mpcg_instance_traits(const mpcg_problem *pr, char *buf, int len);
+
 /* Batched solve, every pointer in device memory, enqueued on `stream`
  * (a hipStream_t, NULL = default stream).  Returns 0 on successful launch. */
 int mpcg_solve_batch_device(const mpcg_problem *pr, int batch,

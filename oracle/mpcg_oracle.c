@@ -493,16 +493,21 @@ void orc_mirror(int n, double *H, double eps) {
         }
 }
 
-/* ORC_KFORM (a second build, test infrastructure for rounding-sensitivity records only:
- * scripts/rounding_proxy.py): the SAME algorithm with the GPU kernel's arithmetic forms
- * -- reciprocal square roots and reciprocal multiplies instead of sqrt and divisions
- * (the 2x2 Cholesky through 1/sqrt(m00) and 1/sqrt(det)), the kernel's operand order in
- * the row residuals and Newton terms -- compiled with FMA contraction.  Not the oracle:
- * the default build is the literal restatement. */
-#ifdef ORC_KFORM
-#define KF 1
-#else
+/* Arithmetic forms.  The default build computes the interior point with the GPU kernel's
+ * arithmetic forms, most of which are HPIPM's / BLASFEO's own: the 2x2 Cholesky through
+ * reciprocal square roots and multiplications by the inverted diagonal (BLASFEO's dpotrf
+ * keeps inv_diag), barrier terms through t_inv = 1/t (HPIPM's Gamma = t_inv lam), the row
+ * residual as D.dz + t - d, the step to the boundary as 1 / max(-dt/t, -dl/l), and the QP's
+ * stationarity residual associated as the kernel's lane sums are.  These are rounding
+ * choices of the same algorithm; they matter where an exit decision rests on rounding
+ * (C5's dual-degenerate QPs, DESIGN.md §3.2: the convergence test there reads a residual
+ * made of cancelling multipliers of 1e13 and more).  -DORC_LITERAL builds the literal
+ * forms (divisions, row-order sums): the second build of the rounding-sensitivity record
+ * (scripts/rounding_proxy.py, tests/test_rounding_record.py). */
+#ifdef ORC_LITERAL
 #define KF 0
+#else
+#define KF 1
 #endif
 
 /* ------------------------------------------------------------------ */
@@ -521,7 +526,7 @@ typedef struct {
     int *hsgn;
     /* Riccati storage */
     double L[NU][NU], Y[NU][NX], P[NX][NX], p[NX], y[NU];
-    double il[NU];  /* ORC_KFORM: reciprocal pivots 1/L_ii */
+    double il[NU];  /* reciprocal pivots 1/L_ii (default build, nu 2) */
     double Hh[NZ][NZ], q[NZ];
     double dz[NZ], ddz[NZ], pi[NX], pin[NX];
 } qp_stage;
@@ -570,6 +575,48 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
             if (fabs(acc) > i_max) i_max = fabs(acc);
             comp += S->lam[c] * S->t[c];
             m++;
+        }
+        if (KF) {
+            /* the kernel's association of the stationarity residual: (H dz + g) + (box
+             * multipliers: upper - lower per variable, plus the h rows' sums per lane part
+             * folded part 0 + part 1 + part 2), then + F' pi term by term, then - pi_prev */
+            const int parts = (64 / (N + 1)) >= 3 ? 3 : 2;
+            double rbox[NZ] = {0}, rh[3][NZ];
+            memset(rh, 0, sizeof rh);
+            for (int c = 0; c < S->ni; c++) {
+                if (S->hrow[c] < 0) {
+                    for (int i = 0; i < NZ; i++)
+                        if (S->D[c][i] != 0.0) rbox[i] += S->D[c][i] * S->lam[c]; /* lower (-l) then upper (+l) */
+                }
+            }
+            for (int i = 0; i < NZ; i++) rbox[i] = rbox[i] == 0.0 ? 0.0 : rbox[i];
+            /* upper - lower in the kernel's operand order */
+            for (int i = 0; i < NZ; i++) {
+                double lo = 0.0, hi = 0.0;
+                for (int c = 0; c < S->ni; c++)
+                    if (S->hrow[c] < 0 && S->D[c][i] != 0.0) { if (S->D[c][i] > 0) hi = S->lam[c]; else lo = S->lam[c]; }
+                rbox[i] = hi - lo;
+            }
+            for (int c = 0; c < S->ni; c++) {
+                if (S->hrow[c] < 0) continue;
+                const int pp = S->hrow[c] % parts;
+                for (int i = 0; i < NZ; i++) rh[pp][i] += S->D[c][i] * S->lam[c];
+            }
+            for (int i = 0; i < NZ; i++) {
+                double acc = rh[0][i];
+                for (int pp = 1; pp < parts; pp++) acc += rh[pp][i];
+                rbox[i] += acc;
+            }
+            for (int i = 0; i < NZ; i++) {
+                double a = 0.0;
+                for (int j = 0; j < NZ; j++) a += S->H[i][j] * S->dz[j];
+                r[i] = a + S->g[i] + rbox[i];
+            }
+            if (k < N)
+                for (int m2 = 0; m2 < NX; m2++)
+                    for (int i = 0; i < NZ; i++) r[i] += (i < NU ? S->B[m2][i] : S->A[m2][i - NU]) * S->pi[m2];
+            if (k > 0)
+                for (int i = 0; i < NX; i++) r[NU + i] -= w->st[k - 1].pi[i];
         }
         int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
         for (int i = i0; i < i1; i++)
@@ -624,7 +671,7 @@ static int riccati_factor(qp_ws *w) {
                 M[i][j] = acc;
             }
         if (KF && NU == 2) {
-            /* kernel: both reciprocal square roots from the block entries,
+            /* both reciprocal square roots from the block entries,
              * 1/l11 = l00 / sqrt(m00 m11 - m10^2) */
             const double m00 = M[0][0], m10 = M[1][0], m11 = M[1][1];
             if (!(m00 > 0.0)) return -1;

@@ -19,6 +19,12 @@ LIB_SLACK = os.path.join(HERE, "libmpcg_oracle_slack.so")
 LIB_BICYCLE = os.path.join(HERE, "libmpcg_oracle_bicycle.so")
 LIBS = {"unicycle": LIB, "unicycle_slack": LIB_SLACK, "bicycle_ca": LIB_BICYCLE}
 MODEL_DIMS = {"unicycle": (5, 2), "unicycle_slack": (6, 2), "bicycle_ca": (6, 3)}
+# the literal-forms builds (-DORC_LITERAL: divisions and row-order sums; mpcg_oracle.c
+# "Arithmetic forms"): the second build of the rounding-sensitivity record
+for _m, _f in (("unicycle", "libmpcg_oracle_literal.so"), ("unicycle_slack", "libmpcg_oracle_slack_literal.so"),
+               ("bicycle_ca", "libmpcg_oracle_bicycle_literal.so")):
+    LIBS[_m + "_literal"] = os.path.join(HERE, _f)
+    MODEL_DIMS[_m + "_literal"] = MODEL_DIMS[_m]
 
 ORC_MAX_NU, ORC_MAX_NX = 3, 6
 
@@ -145,13 +151,14 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
 class Oracle:
     """Thin wrapper: stage functions and full solves on numpy arrays."""
 
-    def __init__(self, layout, **opts):
+    def __init__(self, layout, literal=False, **opts):
+        """literal=True: the literal-forms build (rounding-sensitivity records only)"""
         self.layout = layout
         self.pr = problem_from_layout(layout, **opts)
         self.nx = nx = layout.nx
         self.nu = layout.nu
         self.nz = nx + self.nu
-        self.L = lib(layout.model)
+        self.L = lib(layout.model + ("_literal" if literal else ""))
 
     @property
     def nh(self):

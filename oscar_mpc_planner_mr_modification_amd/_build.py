@@ -49,7 +49,10 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: str = LIB) -> str:
+def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: str = LIB, sources=None) -> str:
+    """libmpcg.so (or a diagnostic / variant build of it with extra_flags at `out`; `sources`
+    restricts the built-in instance files of such a build)"""
+    srcs = SOURCES if sources is None else {k: v for k, v in SOURCES.items() if k in sources}
     deps = [os.path.join(CSRC, s) for s in list(SOURCES) + HEADERS] + [os.path.join(INCLUDE, "mpcg.h"), __file__]
     if not force and not _stale(out, deps):
         return out
@@ -58,7 +61,7 @@ def build_lib(force: bool = False, verbose: bool = False, extra_flags=(), out: s
     os.makedirs(objdir, exist_ok=True)
     common = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}"]
     objs, procs = [], []
-    for src, flags in SOURCES.items():
+    for src, flags in srcs.items():
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         cmd = common + list(flags) + list(extra_flags) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:

@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "mpcg.h"
 #include "mpcg_sqp.h"
 
@@ -25,7 +27,7 @@ typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpc
  * doubles of one solve's QP memory and the workspace bytes of one solve.  Returns 0 (a
  * shape already present keeps its first launcher). */
 int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
-                           int qp_mem_size, long long workspace_bytes_per_solve);
+                           int qp_mem_size, long long workspace_bytes_per_solve, const char* traits);
 }
 
 namespace mpcg {
@@ -47,10 +49,21 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
     return (int)hipGetLastError();
 }
 
+// the storage choices of an instance (mpcg_instance_traits): lane parts per stage, row slots
+// per lane, stored 1/t, LEAN / GFH storage, constant [B A] rows, paired chains, LDS bytes
+template <class C>
+const char* instance_traits() {
+    static char buf[192];
+    snprintf(buf, sizeof buf, "parts=%d slots=%d store_it=%d lean=%d gfh=%d fconst=%d pair=%d lds=%d", C::PARTS,
+             C::SLOTS, (int)C::STORE_IT, (int)lds_lean<C>(), (int)lds_gfh<C>(), (int)C::FCONST, (int)C::PAIR_CHAINS,
+             (int)sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>()>));
+    return buf;
+}
+
 template <class C>
 int register_instance() {
     return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM,
-                                  (long long)(gfh_doubles<C>() * sizeof(double)));
+                                  (long long)(gfh_doubles<C>() * sizeof(double)), instance_traits<C>());
 }
 
 }  // namespace mpcg

@@ -89,6 +89,7 @@ struct Inst {
     mpcg_instance_launch fn = nullptr;
     int qpm = 0;         // doubles of one solve's QP memory (Cfg::QPM)
     long long ws = 0;    // workspace bytes of one solve (GFH stage blocks; 0: none)
+    const char* traits = "";
 };
 static std::mutex& registry_mutex() {
     static std::mutex m;
@@ -194,7 +195,8 @@ static int check_problem(const mpcg_problem* pr, int batch, Inst* inst) {
 }  // namespace mpcg
 
 extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx,
-                                      mpcg_instance_launch fn, int qp_mem_size, long long workspace_bytes_per_solve) {
+                                      mpcg_instance_launch fn, int qp_mem_size, long long workspace_bytes_per_solve,
+                                      const char* traits) {
     if (!fn) return -1;
     std::lock_guard<std::mutex> l(mpcg::registry_mutex());
     for (const mpcg::Inst& in : mpcg::registry())
@@ -205,6 +207,7 @@ extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, in
     in.fn = fn;
     in.qpm = qp_mem_size;
     in.ws = workspace_bytes_per_solve;
+    in.traits = traits ? traits : "";
     mpcg::registry().push_back(in);
     return 0;
 }
@@ -234,6 +237,14 @@ void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps =
 const char* mpcg_last_error(void) { return mpcg::g_err.c_str(); }
 
 int mpcg_supported(const mpcg_problem* pr) { return (pr && mpcg::find_instance(*pr).fn) ? 0 : -1; }
+
+int mpcg_instance_traits(const mpcg_problem* pr, char* buf, int len) {
+    if (!pr || !buf || len < 1) return -1;
+    const mpcg::Inst in = mpcg::find_instance(*pr);
+    if (!in.fn) return -1;
+    std::snprintf(buf, (size_t)len, "%s", in.traits);
+    return 0;
+}
 
 int mpcg_qp_mem_size(const mpcg_problem* pr) {
     if (!pr) return -1;

@@ -75,10 +75,14 @@ struct Cfg {
     static constexpr int NB = (HAS_SLACK && NS > 0) ? 4 : 3;
     static constexpr int NBT = NB * (NB + 1) / 2;
     static constexpr int NDH = NZ + NBT + 1;         // dH: diag | block | zero slot
-    // the bicycle instances run two parts per stage: with three (N <= 20) the N = 10
-    // test instance left parity once its MIRROR was reduced to the 8 coupled
-    // variables (root cause open; the C3 horizon N = 30 has two parts either way)
-    static constexpr int PARTS = MODEL_ == 1 ? 2 : ((64 / (N + 1)) >= 3 ? 3 : 2);
+    // the bicycle instances run two parts per stage (C3's N = 30 allows no more; the
+    // register-starved bicycle keeps its row state small on the short test shapes too).
+    // MPCG_PARTS_BIKE=3 builds three parts where they fit (A/B and parity runs only)
+#ifndef MPCG_PARTS_BIKE
+#define MPCG_PARTS_BIKE 2
+#endif
+    static constexpr int PARTS_MAX = (64 / (N + 1)) >= 3 ? 3 : 2;
+    static constexpr int PARTS = MODEL_ == 1 ? (MPCG_PARTS_BIKE < PARTS_MAX ? MPCG_PARTS_BIKE : PARTS_MAX) : PARTS_MAX;
     static_assert((N + 1) * PARTS <= 64, "horizon too long for one wavefront");
     static_assert(NTRI <= 64, "stage block larger than a wavefront");
     // rows of a lane: box slots j (variable part + PARTS j, lower and upper

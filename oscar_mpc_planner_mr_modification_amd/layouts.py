@@ -263,6 +263,12 @@ def config_layout(cfg: str) -> Layout:
         # (generate_jackalsimulator_solver.py:147) with N 30, max_obstacles 4
         # (mpc_planner_jackalsimulator/config/settings.yaml:3,37); n_paths 4 -> 5 planners (:104)
         return tmpc_layout(N=30, max_obstacles=4, name="JS")
+    if cfg == "JD":
+        # the reference's shipped jackal / dingo solver: configuration_tmpc
+        # (generate_jackal_solver.py:54-75, consistency on: settings.yaml:110) with N 30,
+        # max_obstacles 5 (mpc_planner_jackal/config/settings.yaml:3,38, mpc_planner_dingo :2,33),
+        # n_paths 4 -> 5 planners (:102)
+        return tmpc_layout(N=30, max_obstacles=5, name="JD")
     if cfg == "C5":
         lay = safe_horizon_layout(N=20, n_constraints=24)
         lay.name = "C5"

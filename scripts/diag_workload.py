@@ -51,7 +51,7 @@ def main():
     t0 = time.time()
     b = make_batch(lay, args.scenes, 8, first_scene=args.first, workers=8)
     tg = time.time() - t0
-    orc = oracle_py.Oracle(lay, qp_warm_start=args.ws)
+    orc = oracle_py.Oracle(lay, qp_warm_start=args.ws, qp_warm_first=int(args.ws == 2))
     t0 = time.time()
     r = orc.solve_batch(b.params, b.warm, b.xinit)
     ts = time.time() - t0

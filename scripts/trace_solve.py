@@ -55,7 +55,7 @@ def main():
             "from oscar_mpc_planner_mr_modification_amd.layouts import config_layout; "
             f"lay = config_layout({args.config!r}); d = np.load({os.path.join(ROOT, 'gpurun_out', 'trace_inputs.npz')!r}); "
             "t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to('cuda:0'); "
-            f"o = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start={args.ws}), "
+            f"o = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start={args.ws}, qp_warm_first={int(args.ws == 2)}), "
             "t(d['params']), t(d['warm']), t(d['xinit'])); torch.cuda.synchronize(); "
             "print('GPU exit', o['exit'].cpu().numpy(), 'info', o['info'].cpu().numpy().tolist(), flush=True); "
             "np.save(" + repr(os.path.join(ROOT, "gpurun_out", "trace_gpu_xtraj.npy")) + ", o['xtraj'].cpu().numpy())")
@@ -66,7 +66,7 @@ def main():
     print("==== oracle trace", flush=True)
     i = args.solve
     os.environ["ORC_DEBUG"] = "1"
-    r = oracle_py.Oracle(lay, qp_warm_start=args.ws).solve_batch(b.params[i:i + 1], b.warm[i:i + 1],
+    r = oracle_py.Oracle(lay, qp_warm_start=args.ws, qp_warm_first=int(args.ws == 2)).solve_batch(b.params[i:i + 1], b.warm[i:i + 1],
                                                                  b.xinit[i:i + 1], nthreads=1)
     sys.stderr.flush()
     print("oracle exit", r["status"], "sqp", r["sqp_iter"], "qp", r["qp_iter"], "maxit", r["qp_maxiter"], flush=True)

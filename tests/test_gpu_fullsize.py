@@ -1,25 +1,21 @@
 """Full-size GPU-vs-oracle parity on the bench batches (BASELINE.json configs):
 C2 1024 scenes x 8 guesses, C4 2048 x 8 (one GPU's shard of 16384), C5 2048 x 4
-parallel scenario solvers, C3 4096 bicycle solves, JS (the shipped jackalsimulator
-solver) 4096 x 5, C1 1024 scenes.  Exit codes identical on every solve, trajectories of
-successful solves within 1e-4, and failed solves that took the same path (same
-RTI and interior-point iteration counts on both sides) also within 1e-4.
+parallel scenario solvers started from the previous plan and (C5B) from the braking
+plan, C3 4096 bicycle solves, JS (the shipped jackalsimulator solver) 4096 x 5, JD (the shipped jackal / dingo solver, N 30 with 5 obstacles) 4096 x 5, C1 1024
+scenes; the reference's QP start (qp_solver_warm_start 2, warm_start_first_qp off).
+Exit codes identical on every solve, trajectories of every successful solve within 1e-4
+(north_star), and failed solves that took the same path (same RTI and interior-point
+iteration counts on both sides) also within 1e-4.
 
-C5 exception: the SH-MPC slack state is pinned at 0 by the x0
-bound and its zero dynamics (generate_acados_solver.py:95, solver_model.py:289-292),
-so its lower-bound rows have zero gap at every stage and the QP is dual-degenerate
-(the pinned rows' multipliers and the slack's dynamics multipliers trade along an
-unbounded ray).  On a few QPs the interior point drifts along that ray until the
-multipliers reach 1e13-1e15 and the residuals' rounding floor (one ulp of them) passes
-the tolerance; whether it converges first is decided by rounding, and the solve then
-ends in a QP NaN status on one side.  The test bounds their number and checks that
-every disagreement is of that kind; with the previous-plan warm start (round 2) the exit
-codes agree on the full batch and the same drift shows as a successful copy whose interior
-point took a different path on the two sides."""
+The SH-MPC slack QPs are dual-degenerate: on a few copies the interior
+point's convergence test reads a residual made of cancelling multipliers of 1e13 and more,
+so the exit decision rests on rounding.  The oracle's default build computes the interior
+point with the kernel's arithmetic forms (oracle/mpcg_oracle.c "Arithmetic forms"), which
+makes those decisions the same on both sides; the literal-forms build parts from both on
+such copies (tests/test_rounding_record.py, profiles/r03_rounding_record.json)."""
 import os
 import sys
 
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -28,28 +24,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg", ["C2", "C4", "C5", "C3", "JS", "C1"])
-def test_fullsize_exit_agreement(cfg):
+@pytest.mark.parametrize("cfg", ["C2", "C4", "C5", "C5B", "C3", "JS", "JD", "C1"])
+def test_fullsize_parity(cfg):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from parity_full import DEFAULT_SCENES, compare
 
-    r = compare(cfg, DEFAULT_SCENES[cfg], 0)
+    r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0)
     print(r)
+    assert r["exit_agreement"] == 1.0, r["disagreeing"]
+    assert r["max_abs_dx_success"] <= 1e-4, r["success_dx_over_1e-4"]
     assert r["same_path_failed_dx"] is None or r["same_path_failed_dx"] <= 1e-4
-    assert r["max_abs_dx_success_same_path"] <= 1e-4
-    if cfg != "C5":
-        assert r["max_abs_dx_success"] <= 1e-4
-        assert r["exit_agreement"] == 1.0
-        assert r["success_frac"] >= 0.9, r["success_frac"]
+    floor = {"C5": 0.85, "C5B": 0.55}.get(cfg, 0.9)
+    assert r["success_frac"] >= floor, r["success_frac"]
+    if cfg not in ("C5", "C5B"):
         assert r["rti_iters_per_solve"] >= 9.0
-    else:
-        # rounding decides the interior-point path of the dual-degenerate slack QPs: a few
-        # copies end differently or, both succeeding, on different paths; bounded, and each
-        # one of that kind
-        assert r["exit_agreement"] >= 0.999
-        for d in r["disagreeing"]:
-            assert d["gpu_info"][2] == 1 or d["oracle_qp_status"] == 1, d
-        assert len(r["success_dx_over_1e-4"]) <= 8, r["success_dx_over_1e-4"]
-        for d in r["success_dx_over_1e-4"]:
-            assert not d["same_path"], d
-        assert r["success_frac"] >= 0.85, r["success_frac"]

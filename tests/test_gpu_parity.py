@@ -289,3 +289,24 @@ def test_edge_inputs_empty_nonfinite_unsupported(native, torch_dev, oracle_mod):
     bad.N = 17
     with pytest.raises(RuntimeError, match="no compiled instance"):
         native.solve_batch_device(bad, t(params[:, :17]).contiguous(), t(warm[:, :18]).contiguous(), t(xinit))
+
+
+def test_c5_rounding_decided_copy(native, torch_dev, oracle_mod):
+    """C5 copy 7799 (scene 1949, solver 3): its fifth QP's exit decision rests on the rounding
+    of cancelling multipliers of 1e20 (tests/test_rounding_record.py); the kernel takes the
+    same decision as the oracle's default build (the kernel's arithmetic forms) and ends on
+    the same path."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.scenario import make_shmpc_batch
+
+    lay = config_layout("C5")
+    b = make_shmpc_batch(lay, 1, first_scene=1949)
+    ref = oracle_mod.Oracle(lay).solve_batch(b.params, b.warm, b.xinit)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(torch_dev)  # noqa: E731
+    out = native.solve_batch_device(native.problem_from_layout(lay), t(b.params), t(b.warm), t(b.xinit))
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    np.testing.assert_array_equal(got["exit"], ref["status"])
+    np.testing.assert_array_equal(got["info"][:, 0], ref["sqp_iter"])
+    np.testing.assert_array_equal(got["info"][:, 1], ref["qp_iter"])
+    assert np.abs(got["xtraj"] - ref["xtraj"]).max() <= 1e-9

@@ -55,13 +55,14 @@ def _check(ref, got, label):
 
 @pytest.mark.parametrize("cfg,S,seed", [("C2", 16, 20251212), ("C1", 8, 3)])
 def test_warm_start_parity(native, dev, oracle_mod, cfg, S, seed):
-    """qp_warm_start = 2: every QP after the first starts from its predecessor's solution
-    with slacks and multipliers clipped at qp_ws_thr; GPU == oracle."""
+    """qp_warm_start = 2 with warm_start_first_qp (qp_warm_first): every QP after the first
+    starts from its predecessor's solution with slacks and multipliers clipped at qp_ws_thr;
+    GPU == oracle."""
     lay, b = _batch(cfg, S, seed)
     t = _t(dev)
-    ref = oracle_mod.Oracle(lay, qp_warm_start=2).solve_batch(b.params, b.warm, b.xinit)
-    out = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start=2), t(b.params), t(b.warm),
-                                    t(b.xinit))
+    ref = oracle_mod.Oracle(lay, qp_warm_start=2, qp_warm_first=1).solve_batch(b.params, b.warm, b.xinit)
+    out = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start=2, qp_warm_first=1), t(b.params),
+                                    t(b.warm), t(b.xinit))
     got = {k: v.cpu().numpy() for k, v in out.items()}
     _check(ref, got, f"{cfg} warm start")
     cold = oracle_mod.Oracle(lay, qp_warm_start=0).solve_batch(b.params, b.warm, b.xinit)
@@ -75,8 +76,8 @@ def test_qp_memory_carried_between_solves(native, dev, oracle_mod):
     import torch
     lay, b = _batch("C2", 8, 515)
     t = _t(dev)
-    orc = oracle_mod.Oracle(lay, qp_warm_start=2)
-    pr = native.problem_from_layout(lay, qp_warm_start=2)
+    orc = oracle_mod.Oracle(lay, qp_warm_start=2, qp_warm_first=1)
+    pr = native.problem_from_layout(lay, qp_warm_start=2, qp_warm_first=1)
     ref1 = orc.solve_batch(b.params, b.warm, b.xinit, return_lam=True, return_qp=True)
     out1 = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), lam_out=True, qp_out=True)
     got1 = {k: v.cpu().numpy() for k, v in out1.items()}
@@ -105,9 +106,9 @@ def test_nlp_residual_stats(native, dev, oracle_mod, cfg, ws):
     (stationarity, dynamics, inequality violation, complementarity)."""
     lay, b = _batch(cfg, 4 if cfg != "C5" else 8, 77)
     t = _t(dev)
-    ref = oracle_mod.Oracle(lay, qp_warm_start=ws).solve_batch(b.params, b.warm, b.xinit)
-    out = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start=ws), t(b.params), t(b.warm),
-                                    t(b.xinit), stats=True)
+    ref = oracle_mod.Oracle(lay, qp_warm_start=ws, qp_warm_first=1).solve_batch(b.params, b.warm, b.xinit)
+    out = native.solve_batch_device(native.problem_from_layout(lay, qp_warm_start=ws, qp_warm_first=1), t(b.params),
+                                    t(b.warm), t(b.xinit), stats=True)
     st = out["stats"].cpu().numpy()
     ex = out["exit"].cpu().numpy()
     same = ex == ref["status"]
