@@ -214,13 +214,24 @@ int mpcg_context_set_iterations(mpcg_context *ctx, int sqp_iters);
  *   main_warm      [S][N+1][nvar]    the main solver's warm start, or NULL = braking plan
  *   prev_traj      [S][N][2]         stored previous plan, or NULL
  *   prev_elapsed   [S]               seconds since it was stored (NaN: none)
- *   consistency_on [S][G]            planners with the consistency cost, or NULL */
+ *   consistency_on [S][G]            planners with the consistency cost, or NULL
+ * ABI 6, t-mpc.warmstart_with_mpc_solution (settings.yaml:71; guidance_constraints.cpp:335-338):
+ *   planner_xtraj  [S*G][N+1][nx]    each planner's own previous output (its Solver's _output)
+ *   planner_utraj  [S*G][N][nu]
+ *   existing_guidance [S][G]         the planner's guidance existed in the previous step
+ *   warmstart_with_mpc_solution      1: guided planners with existing guidance start from
+ *                                    initializeWarmstart(state, shift_forward) of their own
+ *                                    previous output instead of the guidance trajectory
+ *   shift_forward                    shift_previous_solution_forward && enable_output */
 typedef struct mpcg_scene_io {
     const double *stage_params, *state, *obst, *obst_meta, *guidance;
     const unsigned char *guided;
     const double *main_warm, *prev_traj, *prev_elapsed;
     const unsigned char *consistency_on;
     double robot_radius, w_consistency, deceleration;
+    const double *planner_xtraj, *planner_utraj;
+    const unsigned char *existing_guidance;
+    int warmstart_with_mpc_solution, shift_forward;
 } mpcg_scene_io;
 
 /* Per-planner solver inputs of one control step on the device: params

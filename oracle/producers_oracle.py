@@ -5,6 +5,8 @@ for the device kernel mpcg_prepare.  Only tests/ may import it.
 One (scene, planner, stage) at a time, following the reference sources:
   braking                acados_solver_interface.cpp:303-342
   guidance warm start    guidance_constraints.cpp:546-570
+  own warm start         t-mpc.warmstart_with_mpc_solution, guidance_constraints.cpp:335-338 ->
+                         Solver::initializeWarmstart, acados_solver_interface.cpp:344-376
   topology halfspaces    linearized_constraints.cpp:49-128 (update), 130-148
                          (projectToSafety), 150-189 (setParameters)
   Douglas-Rachford       ros_tools (external, not in /root/reference): the
@@ -41,7 +43,8 @@ def douglas_rachford(pos, delta, anchor, r):
     return (0.5 * (pos[0] + rb[0]), 0.5 * (pos[1] + rb[1]))
 
 
-def prepare(layout, sc, robot_radius, w_consistency, deceleration=3.0):
+def prepare(layout, sc, robot_radius, w_consistency, deceleration=3.0, warmstart_with_mpc_solution=False,
+            shift_forward=False):
     N, npar, dt = layout.N, layout.npar, layout.dt
     S, G = sc.state.shape[0], sc.guided.shape[1]
     ix = layout.idx
@@ -91,7 +94,25 @@ def prepare(layout, sc, robot_radius, w_consistency, deceleration=3.0):
             b = s * G + g
             guided = bool(sc.guided[s, g])
             w = mw.copy()
-            if guided:
+            own = (guided and warmstart_with_mpc_solution and sc.existing_guidance is not None
+                   and bool(sc.existing_guidance[s, g]))
+            if own:
+                # initializeWarmstart(state, shift) on the copied main solver, from this planner's
+                # own previous output (getOutput reads the local solver's _output)
+                xt, ut = sc.planner_xtraj[b], sc.planner_utraj[b]
+                for k in range(N + 1):
+                    if not shift_forward:
+                        if k < N:
+                            w[k, 0:2] = ut[k]
+                            w[k, 2:7] = xt[k]
+                    elif k == 0:
+                        w[0, 0:2] = ut[1]      # the reference reads State out of range here
+                        w[0, 2:7] = x0
+                    else:
+                        src = N - 1 if k >= N - 1 else k + 1
+                        w[k, 0:2] = ut[src]
+                        w[k, 2:7] = xt[src]
+            elif guided:
                 for k in range(1, N):
                     gx, gy, vx, vy = sc.guidance[s, g, k]
                     w[k, 2], w[k, 3] = gx, gy

@@ -20,7 +20,8 @@ from .layouts import Layout
 class ControlLoop:
     def __init__(self, layout: Layout, scenes, device, robot_radius: float, w_consistency: float,
                  selection_weight: float, deceleration: float = 3.0, shift_forward: bool = False,
-                 consistency_on_non_guided: bool = True, elapsed: float | None = None):
+                 consistency_on_non_guided: bool = True, elapsed: float | None = None,
+                 warmstart_with_mpc_solution: bool = False):
         import torch
 
         self.lay = layout
@@ -29,6 +30,9 @@ class ControlLoop:
         self.S, self.G = scenes.n_scenes, scenes.n_guesses
         self.rr, self.wc, self.sw, self.dec = robot_radius, w_consistency, selection_weight, deceleration
         self.shift, self.cong = shift_forward, consistency_on_non_guided
+        # t-mpc.warmstart_with_mpc_solution (guidance_constraints.cpp:335-338): from the second step on,
+        # guided planners (whose guidance then exists) start from their own previous output
+        self.own_warm = warmstart_with_mpc_solution
         self.elapsed = layout.dt if elapsed is None else elapsed
         self.dsc = native.scenes_to_device(scenes, device)
         LS = 5 + layout.nh
@@ -45,7 +49,11 @@ class ControlLoop:
     def step(self, stream=None):
         """One control step of every scene.  Returns dict(best, exit, xtraj, utraj, pobj, objective, prepared)."""
         pr, S, G, N = self.pr, self.S, self.G, self.lay.N
-        prep = native.prepare_device(pr, self.dsc, self.rr, self.wc, self.dec, stream=stream)
+        if self.own_warm and self.last is not None:
+            self.dsc["planner_xtraj"], self.dsc["planner_utraj"] = self.last["xtraj"], self.last["utraj"]
+            self.dsc["existing_guidance"] = self.dsc["guided"]
+        prep = native.prepare_device(pr, self.dsc, self.rr, self.wc, self.dec, stream=stream,
+                                     warmstart_with_mpc_solution=self.own_warm, shift_forward=self.shift)
         out = native.solve_batch_device(pr, prep["params"], prep["warm"], prep["xinit"], stream=stream,
                                         lam_in=self.lam, lam_out=True)
         best, objective = native.select_best_device(S, G, N, out["xtraj"], out["pobj"], out["exit"],

@@ -99,8 +99,31 @@ __global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scen
         }
     }
     __syncthreads();
+    // t-mpc.warmstart_with_mpc_solution (guidance_constraints.cpp:335-338): a guided planner whose
+    // guidance already existed starts from its own previous output (Solver::initializeWarmstart,
+    // acados_solver_interface.cpp:344-376) on top of the copied main warm start
+    const bool own_warm = guided && in.warmstart_with_mpc_solution && in.existing_guidance && in.planner_xtraj &&
+                          in.planner_utraj && in.existing_guidance[(size_t)sc * G + g];
+    if (own_warm) {
+        const double* xt = in.planner_xtraj + (size_t)sol * (N + 1) * MPCG_NX;
+        const double* ut = in.planner_utraj + (size_t)sol * N * MPCG_NU;
+        for (int e = lane; e < (N + 1) * MPCG_NVAR; e += 64) {
+            const int k = e / MPCG_NVAR, i = e - k * MPCG_NVAR;
+            if (!in.shift_forward) {
+                // [out_0 .. out_{N-1}]; x0[N] stays the copied main warm start
+                if (k < N) (&L.warm[0][0])[e] = i < MPCG_NU ? ut[k * MPCG_NU + i] : xt[k * MPCG_NX + i - MPCG_NU];
+            } else {
+                // [state, out_2, ..., out_{N-1}, out_{N-1}, out_{N-1}]; stage 0's inputs: out_1's (the
+                // reference reads them out of State's range, as in advance_kernel)
+                const int src = k == 0 ? 1 : (k >= N - 1 ? N - 1 : k + 1);
+                (&L.warm[0][0])[e] = i < MPCG_NU ? ut[src * MPCG_NU + i]
+                                                 : (k == 0 ? st[i - MPCG_NU] : xt[src * MPCG_NX + i - MPCG_NU]);
+            }
+        }
+    }
+    __syncthreads();
     // ---- initializeSolverWithGuidance (k = 1..N-1)
-    if (guided && lane >= 1 && lane < N) {
+    if (guided && !own_warm && lane >= 1 && lane < N) {
         const double* gk = in.guidance + (((size_t)sc * G + g) * (N + 1) + lane) * 4;
         L.warm[lane][2] = gk[0];
         L.warm[lane][3] = gk[1];

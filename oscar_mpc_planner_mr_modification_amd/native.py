@@ -272,10 +272,13 @@ def scenes_to_device(scenes, device):
 
 
 def prepare_device(pr: MpcgProblem, dsc: dict, robot_radius: float, w_consistency: float, deceleration: float = 3.0,
-                   out=None, stream=None):
+                   out=None, stream=None, warmstart_with_mpc_solution: bool = False, shift_forward: bool = False):
     """mpcg_prepare: per-planner solver inputs from device-resident scene data
     (`scenes_to_device`).  Returns dict(params, warm, xinit, prev_interp,
-    consistency_active) of device tensors; asynchronous on `stream`."""
+    consistency_active) of device tensors; asynchronous on `stream`.
+    warmstart_with_mpc_solution: guided planners whose dsc["existing_guidance"] is set start
+    from their own previous output dsc["planner_xtraj"] / ["planner_utraj"]
+    (guidance_constraints.cpp:335-338)."""
     import torch
 
     S, G, N = dsc["n_scenes"], dsc["n_guesses"], pr.N
@@ -291,7 +294,9 @@ def prepare_device(pr: MpcgProblem, dsc: dict, robot_radius: float, w_consistenc
     p = lambda k: None if dsc.get(k) is None else dsc[k].data_ptr()  # noqa: E731
     sio = MpcgSceneIo(p("stage_params"), p("state"), p("obst"), p("obst_meta"), p("guidance"), p("guided"),
                       p("main_warm"), p("prev_traj"), p("prev_elapsed"), p("consistency_on"),
-                      float(robot_radius), float(w_consistency), float(deceleration))
+                      float(robot_radius), float(w_consistency), float(deceleration),
+                      p("planner_xtraj"), p("planner_utraj"), p("existing_guidance"),
+                      int(bool(warmstart_with_mpc_solution)), int(bool(shift_forward)))
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     rc = lib.mpcg_prepare(C.byref(pr), S, G, C.byref(sio), _ptr(out["params"]), _ptr(out["warm"]), _ptr(out["xinit"]),
                           _ptr(out["prev_interp"]), _ptr(out["consistency_active"]), C.c_void_p(s.cuda_stream))

@@ -104,7 +104,10 @@ class MpcgSceneIo(C.Structure):
                 ("obst_meta", C.c_void_p), ("guidance", C.c_void_p), ("guided", C.c_void_p),
                 ("main_warm", C.c_void_p), ("prev_traj", C.c_void_p), ("prev_elapsed", C.c_void_p),
                 ("consistency_on", C.c_void_p), ("robot_radius", C.c_double), ("w_consistency", C.c_double),
-                ("deceleration", C.c_double)]
+                ("deceleration", C.c_double),
+                # ABI 6: t-mpc.warmstart_with_mpc_solution
+                ("planner_xtraj", C.c_void_p), ("planner_utraj", C.c_void_p), ("existing_guidance", C.c_void_p),
+                ("warmstart_with_mpc_solution", C.c_int), ("shift_forward", C.c_int)]
 
 
 class MpcgStepIo(C.Structure):

@@ -76,6 +76,11 @@ class Scenes:
     consistency_on: np.ndarray
     previously_selected: np.ndarray
     main_warm: Optional[np.ndarray] = None
+    # t-mpc.warmstart_with_mpc_solution (guidance_constraints.cpp:335-338): each planner's own
+    # previous output and whether its guidance existed in the previous step
+    planner_xtraj: Optional[np.ndarray] = None      # (S*G, N+1, 5)
+    planner_utraj: Optional[np.ndarray] = None      # (S*G, N, 2)
+    existing_guidance: Optional[np.ndarray] = None  # (S, G) bool
 
     @property
     def n_scenes(self) -> int:
@@ -168,18 +173,49 @@ def interpolate_prev(prev: np.ndarray, elapsed: np.ndarray, dt: float):
     return out, valid
 
 
+def initialize_warmstart(warm, xtraj, utraj, state, shift_forward: bool):
+    """Solver::initializeWarmstart(state, shift) (acados_solver_interface.cpp:344-376) on a
+    copied warm start `warm` (N+1, 7) from the solver's own previous output: keep ->
+    [out_0 .. out_{N-1}] with x0[N] unchanged; shift -> [state, out_2, .., out_{N-1},
+    out_{N-1}, out_{N-1}] (stage 0's inputs: out_1's, the reference reads them out of
+    State's range)"""
+    N = utraj.shape[0]
+    w = np.array(warm, float)
+    for k in range(N + 1):
+        if not shift_forward:
+            if k < N:
+                w[k, :2], w[k, 2:] = utraj[k], xtraj[k]
+        else:
+            src = 1 if k == 0 else (N - 1 if k >= N - 1 else k + 1)
+            w[k, :2] = utraj[src]
+            w[k, 2:] = state if k == 0 else xtraj[src]
+    return w
+
+
 def prepare_host(layout: Layout, sc: Scenes, robot_radius: float, w_consistency: float,
-                 deceleration: float = 3.0) -> Prepared:
+                 deceleration: float = 3.0, warmstart_with_mpc_solution: bool = False,
+                 shift_forward: bool = False) -> Prepared:
     N, npar, dt = layout.N, layout.npar, layout.dt
     S, G = sc.n_scenes, sc.n_guesses
     ix = layout.idx
     main = braking(sc.state, N, dt, deceleration) if sc.main_warm is None else np.array(sc.main_warm, float)
     params = np.repeat(np.repeat(sc.stage_params[:, None, None, :], G, 1), N, 2)  # (S, G, N, npar)
     warm = np.repeat(main[:, None], G, 1).copy()                                    # (S, G, N+1, 7)
+    # t-mpc.warmstart_with_mpc_solution: guided planners with existing guidance start from their
+    # own previous output (guidance_constraints.cpp:335-338)
+    own = np.zeros((S, G), bool)
+    if warmstart_with_mpc_solution and sc.existing_guidance is not None and sc.planner_xtraj is not None:
+        own = np.asarray(sc.guided, bool) & np.asarray(sc.existing_guidance, bool)
+        for s_ in range(S):
+            for g_ in range(G):
+                if own[s_, g_]:
+                    b = s_ * G + g_
+                    warm[s_, g_] = initialize_warmstart(warm[s_, g_], sc.planner_xtraj[b], sc.planner_utraj[b],
+                                                        sc.state[s_], shift_forward)
     # initializeSolverWithGuidance: k = 1..N-1
     gd = sc.guidance
     for k in range(1, N):
-        g = sc.guided
+        g = sc.guided & ~own
         warm[:, :, k, 2] = np.where(g, gd[:, :, k, 0], warm[:, :, k, 2])
         warm[:, :, k, 3] = np.where(g, gd[:, :, k, 1], warm[:, :, k, 3])
         warm[:, :, k, 4] = np.where(g, np.arctan2(gd[:, :, k, 3], gd[:, :, k, 2]), warm[:, :, k, 4])

@@ -25,17 +25,23 @@ def _next_state(xtraj, best, state, G):
     return nxt
 
 
-def cpu_loop(lay, sc, steps, oracle_mod, prod_oracle):
+def cpu_loop(lay, sc, steps, oracle_mod, prod_oracle, own_warm=False):
     S, G, N = sc.n_scenes, sc.n_guesses, lay.N
     orc = oracle_mod.Oracle(lay)
     lam = np.zeros((S * G, N, 5 + lay.nh))
     hist = []
+    prev = None
     for _ in range(steps):
-        p = prod_oracle.prepare(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION)
+        if own_warm and prev is not None:
+            # t-mpc.warmstart_with_mpc_solution: every guided planner's guidance existed last step
+            sc.planner_xtraj, sc.planner_utraj = prev["xtraj"], prev["utraj"]
+            sc.existing_guidance = sc.guided.copy()
+        p = prod_oracle.prepare(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION, warmstart_with_mpc_solution=own_warm)
         r = orc.solve_batch(p["params"], p["warm"], p["xinit"], lam_in=lam, return_lam=True)
         best, obj = find_best_planner_host(S, G, N, r["xtraj"], r["pobj"], r["status"], p["prev_interp"], W_CONS,
                                            p["consistency_active"], sc.previously_selected.reshape(-1), SEL_W)
         hist.append(dict(best=best, exit=r["status"], xtraj=r["xtraj"]))
+        prev = r
         sn = _next_state(r["xtraj"], best, sc.state, G)
         c = producers.advance_host(lay, best, r["status"], r["xtraj"], r["utraj"], p["warm"], r["lam"], sn,
                                    sc.guided, lay.dt, DECELERATION, previously_selected=sc.previously_selected)
@@ -73,8 +79,12 @@ def test_cpu_loop_bookkeeping(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,S,G,n_obs", [("C2", 6, 8, None), ("C1", 4, 5, 3)])
-def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs):
+@pytest.mark.parametrize("cfg,S,G,n_obs,own_warm", [("C2", 6, 8, None, False), ("C1", 4, 5, 3, False),
+                                                    ("C2", 6, 8, None, True)])
+def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs, own_warm):
+    """own_warm: t-mpc.warmstart_with_mpc_solution on (guidance_constraints.cpp:335-338)"""
+    import copy
+
     import producers_oracle
     import torch
     from oscar_mpc_planner_mr_modification_amd.control_loop import ControlLoop
@@ -82,9 +92,9 @@ def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs):
     lay = config_layout(cfg)
     steps = 3
     sc0 = make_scenes(lay, S, G, n_obs=n_obs, seed=2024)
-    ref = cpu_loop(lay, sc0, steps, oracle_mod, producers_oracle)
+    ref = cpu_loop(lay, copy.deepcopy(sc0), steps, oracle_mod, producers_oracle, own_warm=own_warm)
     dev = torch.device("cuda:0")
-    loop = ControlLoop(lay, sc0, dev, ROBOT_RADIUS, W_CONS, SEL_W, DECELERATION)
+    loop = ControlLoop(lay, sc0, dev, ROBOT_RADIUS, W_CONS, SEL_W, DECELERATION, warmstart_with_mpc_solution=own_warm)
     sc = sc0
     for t in range(steps):
         out = loop.step()

@@ -39,6 +39,51 @@ def test_host_producers_match_oracle(prod_oracle, cfg, S, G, n_obs):
     assert not ref["consistency_active"].reshape(S, G)[-1].any()
 
 
+def _own_warm_inputs(lay, sc, seed):
+    """each planner's previous output (a perturbed copy of its guidance-started warm start) and a
+    random existing-guidance pattern"""
+    rng = np.random.default_rng(seed)
+    S, G, N = sc.n_scenes, sc.n_guesses, lay.N
+    base = producers.prepare_host(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION).warm
+    sc.planner_xtraj = base[:, :, 2:] + rng.normal(0, 0.05, (S * G, N + 1, 5))
+    sc.planner_utraj = base[:, :N, :2] + rng.normal(0, 0.05, (S * G, N, 2))
+    sc.existing_guidance = rng.uniform(size=(S, G)) < 0.6
+    return sc
+
+
+@pytest.mark.parametrize("shift", [False, True])
+def test_own_warm_start_matches_oracle(prod_oracle, shift):
+    """t-mpc.warmstart_with_mpc_solution (guidance_constraints.cpp:335-338): guided planners with
+    existing guidance start from initializeWarmstart(state, shift) of their own previous output;
+    the others from the guidance (guided) or the main warm start (non-guided)"""
+    lay, sc = _scenes("C2", 3, 8, 77)
+    sc = _own_warm_inputs(lay, sc, 5)
+    host = producers.prepare_host(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION, warmstart_with_mpc_solution=True,
+                                  shift_forward=shift)
+    ref = prod_oracle.prepare(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION, warmstart_with_mpc_solution=True,
+                              shift_forward=shift)
+    np.testing.assert_array_equal(host.params, ref["params"])
+    np.testing.assert_allclose(host.warm, ref["warm"], rtol=0, atol=1e-13)
+    N = lay.N
+    for s in range(3):
+        for g in range(8):
+            b = s * 8 + g
+            if sc.guided[s, g] and sc.existing_guidance[s, g]:
+                if shift:
+                    np.testing.assert_array_equal(host.warm[b, 0, 2:], sc.state[s])
+                    np.testing.assert_array_equal(host.warm[b, 1, 2:], sc.planner_xtraj[b, 2])
+                    np.testing.assert_array_equal(host.warm[b, N, 2:], sc.planner_xtraj[b, N - 1])
+                else:
+                    np.testing.assert_array_equal(host.warm[b, :N, 2:], sc.planner_xtraj[b, :N])
+            elif sc.guided[s, g]:
+                np.testing.assert_array_equal(host.warm[b, 1:N, 2:4], sc.guidance[s, g, 1:N, 0:2])
+    # flag off (the shipped value, settings.yaml:71): every guided planner starts from its guidance
+    off = producers.prepare_host(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION)
+    for s in range(3):
+        for g in range(7):
+            np.testing.assert_array_equal(off.warm[s * 8 + g, 1:N, 2:4], sc.guidance[s, g, 1:N, 0:2])
+
+
 def test_douglas_rachford_step_properties(prod_oracle):
     """Properties of one step of douglasRachfordProjection(p, delta, anchor, r, p):
     a point outside both discs is a fixed point; with delta == anchor a point
@@ -106,4 +151,27 @@ def test_device_prepare_matches_oracle(prod_oracle, cfg, S, G, n_obs):
     np.testing.assert_array_equal(got["consistency_active"].astype(bool), ref["consistency_active"])
     np.testing.assert_array_equal(got["xinit"], ref["xinit"])
     # warm start: cos/sin (braking) and atan2 (guidance heading) may differ in the last ulp
+    np.testing.assert_allclose(got["warm"], ref["warm"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [False, True])
+def test_device_own_warm_start_matches_oracle(prod_oracle, shift):
+    import torch
+    from oscar_mpc_planner_mr_modification_amd import native
+
+    lay, sc = _scenes("C2", 8, 8, 91)
+    sc = _own_warm_inputs(lay, sc, 17)
+    ref = prod_oracle.prepare(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION, warmstart_with_mpc_solution=True,
+                              shift_forward=shift)
+    dev = torch.device("cuda:0")
+    dsc = native.scenes_to_device(sc, dev)
+    t = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(device=dev, dtype=dt)  # noqa: E731
+    dsc["planner_xtraj"], dsc["planner_utraj"] = t(sc.planner_xtraj), t(sc.planner_utraj)
+    dsc["existing_guidance"] = t(sc.existing_guidance.astype(np.uint8), torch.uint8)
+    out = native.prepare_device(native.problem_from_layout(lay), dsc, ROBOT_RADIUS, W_CONS, DECELERATION,
+                                warmstart_with_mpc_solution=True, shift_forward=shift)
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    np.testing.assert_array_equal(got["params"], ref["params"])
     np.testing.assert_allclose(got["warm"], ref["warm"], rtol=0, atol=1e-12)
