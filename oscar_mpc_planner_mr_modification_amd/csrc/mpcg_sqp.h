@@ -1055,9 +1055,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             comp = wave_sum(comp);
             const double mu = comp / C::M_TOTAL;
 #ifdef MPCG_TRACE
-            // diagnostic build only (scripts/trace_solve.py): the oracle's ORC_DEBUG line of solve MPCG_TRACE
-            if (sol == MPCG_TRACE && lane == 0)
-                printf("  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", qit, rs, re, ri, mu);
+            // diagnostic build only (scripts/trace_solve.py): the oracle's ORC_DEBUG line of solve
+            // MPCG_TRACE (-1: every solve, prefixed with its index)
+            if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0)
+                printf("[%d]  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", sol, qit, rs, re, ri, mu);
 #endif
             if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { qstat = AC_NAN; break; }
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
@@ -1369,7 +1370,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         wave_sync();
                         STAMP_LAP(19);
                     }
-                    if (FAC_FLAT ? __any(fbad) : S.flag != 0) { qstat = AC_NAN; break; }
+                    if (FAC_FLAT ? __any(fbad) : S.flag != 0) {
+#ifdef MPCG_TRACE
+                        if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0) printf("[%d]  pivot failed\n", sol);
+#endif
+                        qstat = AC_NAN;
+                        break;
+                    }
                 }
                 STAMP_END(4);
                 // ---- vector + forward passes: affine 5-vector recursions in SGPRs

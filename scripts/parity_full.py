@@ -77,6 +77,17 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
     # the path, and the trajectories then differ by more than rounding
     path_ok = ok & (got["info"][:, 1] == ref["qp_iter"]) & ((got["info"][:, 3] > 0) == (ref["qp_maxiter"] > 0))
     over = np.flatnonzero(ok & (dx > 1e-4))
+    # the literal-forms oracle build (a second legal rounding of the same algorithm): copies on
+    # which the two builds part (exit code, or successful trajectories more than 1e-4 apart) are
+    # rounding-decided -- on those the GPU must end like one of the two builds; everywhere else
+    # it is held to the default build at the north_star bar
+    lit = oracle_py.Oracle(lay, literal=True, qp_warm_start=ws, qp_warm_first=warm_first).solve_batch(
+        b.params, b.warm, b.xinit, nthreads=16)
+    dxl = np.abs(lit["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
+    decided = (lit["status"] != ref["status"]) | ((ref["status"] == 1) & (dxl > 1e-4))
+    det = ~decided
+    dx_lit = np.abs(got["xtraj"] - lit["xtraj"]).reshape(len(same), -1).max(1)
+    ends_like_a_build = ((got["exit"] == ref["status"]) | (got["exit"] == lit["status"]))
     return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "oracle": "literal" if literal else "default",
             "solves": int(len(same)), "exit_agreement": float(same.mean()),
             "max_abs_dx_success_same_path": float(dx[path_ok].max()) if path_ok.any() else None,
@@ -98,7 +109,15 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
             "disagreeing": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
                              "gpu_info": got["info"][i].tolist(), "oracle_sqp": int(ref["sqp_iter"][i]),
                              "oracle_qp_status": int(ref["qp_status"][i])} for i in dis[:20]],
-            "oracle_s": round(t_orc, 2)}
+            "oracle_s": round(t_orc, 2),
+            "rounding_decided": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
+                                  "oracle_literal": int(lit["status"][i]), "gpu_info": got["info"][i].tolist(),
+                                  "builds_dx": float(dxl[i]), "gpu_dx_default": float(dx[i]),
+                                  "gpu_dx_literal": float(dx_lit[i])} for i in np.flatnonzero(decided)[:40]],
+            "n_rounding_decided": int(decided.sum()),
+            "determined_exit_agreement": float(same[det].mean()) if det.any() else None,
+            "determined_max_abs_dx_success": float(dx[det & ok].max()) if (det & ok).any() else None,
+            "rounding_decided_end_like_a_build": bool(ends_like_a_build[decided].all())}
 
 
 def main():

@@ -19,8 +19,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "scripts"
 TRACE_DIR = os.path.join(ROOT, "oscar_mpc_planner_mr_modification_amd", "build", "trace")
 
 
-def lib_path(solve):
-    return os.path.join(TRACE_DIR, f"libmpcg_trace{solve}.so")
+def lib_path(solve=-1):
+    return os.path.join(TRACE_DIR, "libmpcg_trace.so" if solve < 0 else f"libmpcg_trace{solve}.so")
 
 
 def scene_inputs(cfg, scene, braking):
@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--config", default="C5")
     ap.add_argument("--scene", type=int, default=1949)
     ap.add_argument("--solve", type=int, default=3, help="solve index inside the scene's batch")
+    ap.add_argument("--lib-solve", type=int, default=-1, help="the trace build's MPCG_TRACE (-1: every solve)")
     ap.add_argument("--braking", action="store_true")
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--ws", type=int, default=0)
@@ -45,7 +46,7 @@ def main():
     if args.build_only:
         from oscar_mpc_planner_mr_modification_amd import _build
         os.makedirs(TRACE_DIR, exist_ok=True)
-        print(_build.build_lib(force=True, extra_flags=[f"-DMPCG_TRACE={args.solve}"], out=lib_path(args.solve)))
+        print(_build.build_lib(force=True, extra_flags=[f"-DMPCG_TRACE={args.lib_solve}"], out=lib_path(args.lib_solve)))
         return
     lay, b = scene_inputs(args.config, args.scene, args.braking)
     np.savez(os.path.join(ROOT, "gpurun_out", "trace_inputs.npz"), params=b.params, warm=b.warm, xinit=b.xinit)
@@ -59,7 +60,7 @@ def main():
             "t(d['params']), t(d['warm']), t(d['xinit'])); torch.cuda.synchronize(); "
             "print('GPU exit', o['exit'].cpu().numpy(), 'info', o['info'].cpu().numpy().tolist(), flush=True); "
             "np.save(" + repr(os.path.join(ROOT, "gpurun_out", "trace_gpu_xtraj.npy")) + ", o['xtraj'].cpu().numpy())")
-    env = dict(os.environ, MPCG_LIB=lib_path(args.solve))
+    env = dict(os.environ, MPCG_LIB=lib_path(args.lib_solve))
     print("==== GPU trace", flush=True)
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
     import oracle_py
