@@ -380,10 +380,35 @@ struct Rows {
 
 // The rows of the lane (stage k, part p): box slot j <-> variable v(j) = p + PARTS j,
 // h slot r <-> h row hh(r) = p + PARTS r.
+// MPCG_BOUNDS_SEL: the box bounds of a lane's variables are selected from the uniform problem
+// arguments by the lane's part at each use (two v_cndmask per bound) instead of living in
+// 2 BVS VGPR pairs for the whole solve (A/B switch: the register-starved C3 spills them and
+// reloads them in every residual pass)
+#ifndef MPCG_BOUNDS_SEL
+#define MPCG_BOUNDS_SEL 0
+#endif
 template <class C>
 struct LaneRows {
     int k, part;
+#if MPCG_BOUNDS_SEL
+    const mpcg_problem* prb;
+    __device__ __forceinline__ static double bnd(const mpcg_problem& p, int v, bool upper) {
+        if (v >= C::NZ) return 0.0;
+        return v < C::NU ? (upper ? p.ubu[v] : p.lbu[v]) : (upper ? p.ubx[v - C::NU] : p.lbx[v - C::NU]);
+    }
+    __device__ __forceinline__ double sel(int j, bool upper) const {
+        double b = bnd(*prb, C::PARTS * j, upper);
+#pragma unroll
+        for (int q = 1; q < C::PARTS; ++q) b = part == q ? bnd(*prb, q + C::PARTS * j, upper) : b;
+        return b;
+    }
+    __device__ __forceinline__ double lo_at(int j) const { return sel(j, false); }
+    __device__ __forceinline__ double hi_at(int j) const { return sel(j, true); }
+#else
     double lo[C::BVS], hi[C::BVS];
+    __device__ __forceinline__ double lo_at(int j) const { return lo[j]; }
+    __device__ __forceinline__ double hi_at(int j) const { return hi[j]; }
+#endif
     __device__ __forceinline__ int var(int j) const { return part + C::PARTS * j; }
     __device__ __forceinline__ int hrow(int r) const { return part + C::PARTS * r; }
     // input bounds on every stage < N, state bounds on 1..N-1
@@ -535,6 +560,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     LaneRows<C> LR;
     LR.k = k;
     LR.part = part;
+#if MPCG_BOUNDS_SEL
+    LR.prb = &pr;
+#else
 #pragma unroll
     for (int j = 0; j < BVS; ++j) {
         const int v = LR.var(j);
@@ -545,6 +573,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         LR.lo[j] = lo;
         LR.hi[j] = hi;
     }
+#endif
     // gradient (x, y, psi) and gap of h row hh of this lane's stage
     auto rowg = [&](int hh, double& a, double& b, double& c) {
         if constexpr (C::LIN_PARAMS) {
@@ -816,7 +845,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 double lb = 0.0;
                 if (LR.box_on(j)) {
                     const double zv = S.z[k][LR.var(j)];
-                    const double gl = zv - LR.lo[j], gh = LR.hi[j] - zv;
+                    const double gl = zv - LR.lo_at(j), gh = LR.hi_at(j) - zv;
                     const double ll = have_qp ? R.l[2 * j] : 0.0, lh = have_qp ? R.l[2 * j + 1] : 0.0;
                     vin = fmax(vin, -gl);
                     vin = fmax(vin, -gh);
@@ -918,8 +947,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             for (int j = 0; j < BVS; ++j) {
                 const bool on = LR.box_on(j);
                 const double zv = S.z[ks][on ? LR.var(j) : 0];
-                cold(2 * j, on ? zv - LR.lo[j] : 1.0);
-                cold(2 * j + 1, on ? LR.hi[j] - zv : 1.0);
+                cold(2 * j, on ? zv - LR.lo_at(j) : 1.0);
+                cold(2 * j + 1, on ? LR.hi_at(j) - zv : 1.0);
             }
 #pragma unroll
             for (int r = 0; r < HS; ++r) {
@@ -970,8 +999,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const int v = LR.var(j);
                         const double zv = S.z[k][v], dzv = S.dz[k][v];
                         rb = R.l[2 * j + 1] - R.l[2 * j];
-                        row_res(2 * j, -dzv, zv - LR.lo[j]);
-                        row_res(2 * j + 1, dzv, LR.hi[j] - zv);
+                        row_res(2 * j, -dzv, zv - LR.lo_at(j));
+                        row_res(2 * j + 1, dzv, LR.hi_at(j) - zv);
                     } else {
                         R.rin[2 * j] = R.rin[2 * j + 1] = 0.0;
                         R.set_it(2 * j, 1.0);

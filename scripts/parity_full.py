@@ -38,11 +38,12 @@ def inputs(cfg, S, first=0):
     return lay, b
 
 
-def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
+def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQP_RTI"):
     """GPU vs oracle on the bench batch; ws / warm_first: qp_solver_warm_start and
     warm_start_first_qp (default: warm-start the first QP too when ws == 2, the restated
     warm start; ws 2 with warm_first 0 is the reference's configuration, cold in SQP-RTI);
-    literal: compare against the literal-forms oracle build instead"""
+    literal: compare against the literal-forms oracle build instead; solver_type "SQP": one
+    full acados SQP call per solve"""
     if warm_first is None:
         warm_first = int(ws == 2)
     import torch
@@ -53,13 +54,13 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
     lay, b = inputs(cfg, S, first)
     dev = torch.device("cuda:0")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    pr = native.problem_from_layout(lay, qp_warm_start=ws, qp_warm_first=warm_first)
+    opts = dict(qp_warm_start=ws, qp_warm_first=warm_first, solver_type=solver_type)
+    pr = native.problem_from_layout(lay, **opts)
     out = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), stats=True)
     torch.cuda.synchronize()
     got = {k: v.cpu().numpy() for k, v in out.items()}
     t0 = time.time()
-    ref = oracle_py.Oracle(lay, literal=literal, qp_warm_start=ws, qp_warm_first=warm_first).solve_batch(
-        b.params, b.warm, b.xinit, nthreads=16)
+    ref = oracle_py.Oracle(lay, literal=literal, **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
     t_orc = time.time() - t0
     same = got["exit"] == ref["status"]
     ok = same & (got["exit"] == 1)
@@ -81,14 +82,16 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
     # which the two builds part (exit code, or successful trajectories more than 1e-4 apart) are
     # rounding-decided -- on those the GPU must end like one of the two builds; everywhere else
     # it is held to the default build at the north_star bar
-    lit = oracle_py.Oracle(lay, literal=True, qp_warm_start=ws, qp_warm_first=warm_first).solve_batch(
-        b.params, b.warm, b.xinit, nthreads=16)
+    lit = oracle_py.Oracle(lay, literal=True, **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
     dxl = np.abs(lit["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
     decided = (lit["status"] != ref["status"]) | ((ref["status"] == 1) & (dxl > 1e-4))
     det = ~decided
     dx_lit = np.abs(got["xtraj"] - lit["xtraj"]).reshape(len(same), -1).max(1)
     ends_like_a_build = ((got["exit"] == ref["status"]) | (got["exit"] == lit["status"]))
-    return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "oracle": "literal" if literal else "default",
+    capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
+    return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "solver_type": solver_type,
+            "oracle": "literal" if literal else "default",
+            "sqp_iter_agreement": float((got["info"][:, 0] == ref["sqp_iter"]).mean()),
             "solves": int(len(same)), "exit_agreement": float(same.mean()),
             "max_abs_dx_success_same_path": float(dx[path_ok].max()) if path_ok.any() else None,
             "success_solves_other_path": int((ok & ~path_ok).sum()),
@@ -117,7 +120,13 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False):
             "n_rounding_decided": int(decided.sum()),
             "determined_exit_agreement": float(same[det].mean()) if det.any() else None,
             "determined_max_abs_dx_success": float(dx[det & ok].max()) if (det & ok).any() else None,
-            "rounding_decided_end_like_a_build": bool(ends_like_a_build[decided].all())}
+            "rounding_decided_end_like_a_build": bool(ends_like_a_build[decided].all()),
+            # solves in which no QP stopped at the 50-iteration cap on either side: every applied
+            # step is a converged QP solution (a capped QP's step is wherever its stalled interior
+            # point stood; with the warm start and in full SQP the next QPs start from it)
+            "capfree_frac": float(capfree.mean()),
+            "capfree_exit_agreement": float(same[capfree].mean()) if capfree.any() else None,
+            "capfree_max_abs_dx_success": float(dx[capfree & ok].max()) if (capfree & ok).any() else None}
 
 
 def main():
@@ -127,10 +136,12 @@ def main():
     ap.add_argument("--scenes", type=int, default=None)
     ap.add_argument("--warm-first", type=int, default=None)
     ap.add_argument("--literal", action="store_true", help="against the literal-forms oracle build")
+    ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"))
     args = ap.parse_args()
     for cfg in args.configs.split(","):
         for ws in (int(w) for w in args.ws.split(",")):
-            r = compare(cfg, args.scenes or DEFAULT_SCENES[cfg], ws, warm_first=args.warm_first, literal=args.literal)
+            r = compare(cfg, args.scenes or DEFAULT_SCENES[cfg], ws, warm_first=args.warm_first, literal=args.literal,
+                        solver_type=args.solver_type)
             print(json.dumps(r), flush=True)
 
 
