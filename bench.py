@@ -194,7 +194,8 @@ class TmpcWorkload(Workload):
         self.gen_s = time.time() - t0
         self.scenes = self.batch.scenes
         self.dsc = native.scenes_to_device(self.scenes, dev)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first,
+                                             solver_type=args.solver_type)
         B = self.B
         f64 = dict(dtype=torch.float64, device=dev)
         self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, 7), **f64),
@@ -260,7 +261,8 @@ class C3Workload(Workload):
         self.gen_s = time.time() - t0
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_par, self.d_warm, self.d_xi = t(self.b.params), t(self.b.warm), t(self.b.xinit)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first,
+                                             solver_type=args.solver_type)
         f64 = dict(dtype=torch.float64, device=dev)
         self.out = dict(xtraj=torch.empty((S, N + 1, nx), **f64), utraj=torch.empty((S, N, nu), **f64),
                         pobj=torch.empty((S,), **f64), exit=torch.empty((S,), dtype=torch.int32, device=dev),
@@ -329,7 +331,8 @@ class ShmpcWorkload(Workload):
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_sp, self.d_st, self.d_smp = t(self.scenes.stage_params), t(self.scenes.state), t(self.scenes.samples)
         self.d_mw = t(self.scenes.main_warm)   # the main solver's previous plan (scenario.previous_plan)
-        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
+        self.pr = native.problem_from_layout(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first,
+                                             solver_type=args.solver_type)
         B = self.B
         f64 = dict(dtype=torch.float64, device=dev)
         self.prep = dict(params=torch.empty((B, N, lay.npar), **f64), warm=torch.empty((B, N + 1, lay.nvar), **f64),
@@ -426,6 +429,9 @@ def main():
     ap.add_argument("--guesses", type=int, default=None, help="planners per scene (8; JS: 5)")
     ap.add_argument("--qp-warm-start", type=int, default=2, choices=(0, 2),
                     help="qp_solver_warm_start: 2 (the reference's, generate_acados_solver.py:173) or 0 cold")
+    ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"),
+                    help="solver_settings.acados.solver_type: SQP_RTI (default, every shipped config) or SQP "
+                         "(one full acados SQP call per solve, DESIGN.md §2)")
     ap.add_argument("--qp-warm-first", type=int, default=0, choices=(0, 1),
                     help="acados warm_start_first_qp: 0 (default: every SQP-RTI QP starts cold), 1 warm-start "
                          "the first QP of each call too (DESIGN.md §2 'QP start')")
@@ -554,7 +560,7 @@ def main():
     ok = exit_h == 1
     stats = {"success_frac": float(ok.mean()), "rti_iters_per_solve": float(info_h[:, 0].mean()),
              "qp_iters_per_solve": float(info_h[:, 1].mean()), "qp_warm_start": args.qp_warm_start,
-             "qp_warm_first": args.qp_warm_first,
+             "qp_warm_first": args.qp_warm_first, "solver_type": args.solver_type,
              "scene_gen_s": round(wl.gen_s, 2)}
     if isinstance(wl, ShmpcWorkload):
         stats["scene_feasible_frac"] = float((wl.best.cpu().numpy() >= 0).mean())
@@ -588,7 +594,8 @@ def main():
         import oracle_py
 
         oracle_py.build()
-        orc = oracle_py.Oracle(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first)
+        orc = oracle_py.Oracle(lay, qp_warm_start=args.qp_warm_start, qp_warm_first=args.qp_warm_first,
+                                             solver_type=args.solver_type)
         threads = wl.threads
         if world == 1:
             # CPU baseline: chunks of the same batch until ~cpu_seconds of CPU work, checked on the way

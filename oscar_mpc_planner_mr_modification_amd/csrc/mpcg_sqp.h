@@ -90,19 +90,16 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
-    // 1/t of every row kept in registers when the row state is small; the two-part
-    // instances (long horizons, more rows per lane) recompute it.  (A two-part instance
-    // with stored 1/t -- N 30 with 4 obstacles, SLOTS 12 -- computed wrong trajectories and
-    // once faulted on the GPU in round 2; the two-part shape of C4, which recomputes 1/t,
-    // is the one validated at full size.)
+    // 1/t of every row kept in registers when the row state is small (up to 14 slots: C1, C2,
+    // C5, JS, JD); the instances with more row slots per lane (C4 20, C3 16) recompute it, which
+    // keeps them out of scratch.  Measured (scripts/ab_bench.py, profiles/r03d_ab_*): JS 42.11 ->
+    // 41.39 ms, C5 20.89 -> 20.68, JD unchanged; the stored variant of the two-part instances
+    // passed full-size parity (JS, JD: 20,480 solves each, profiles/r03c_variant_storeit.jsonl).
+    // MPCG_STORE_IT_MAX=0 recomputes it everywhere.
 #ifndef MPCG_STORE_IT_MAX
-#define MPCG_STORE_IT_MAX 12
+#define MPCG_STORE_IT_MAX 14
 #endif
-#ifdef MPCG_STORE_IT_ANY
     static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
-#else
-    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX && PARTS == 3;
-#endif
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     // Linear rows (topology and scenario halfspaces) read their coefficients from the
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
