@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="C1")
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--guesses", type=int, default=8)
+    ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"))
     args = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime before libmpcg.so)
     from oscar_mpc_planner_mr_modification_amd import native
@@ -31,8 +32,8 @@ def main():
 
     lay = config_layout(args.config)
     b = make_batch(lay, 4, args.guesses, seed=99)
-    pr = native.problem_from_layout(lay)
-    out = {"config": args.config, "N": lay.N, "obstacles": lay.max_obstacles}
+    pr = native.problem_from_layout(lay, solver_type=args.solver_type)
+    out = {"config": args.config, "N": lay.N, "obstacles": lay.max_obstacles, "solver_type": args.solver_type}
     for batch in (1, args.guesses):
         ctx = native.Context(pr, batch)
         P, W, X = b.params[:batch], b.warm[:batch], b.xinit[:batch]
@@ -48,7 +49,7 @@ def main():
         ctx.close()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
-    orc = oracle_py.Oracle(lay)
+    orc = oracle_py.Oracle(lay, solver_type=args.solver_type)
     ts = []
     for i in range(min(args.reps, 50)):
         t0 = time.perf_counter()
