@@ -50,13 +50,16 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
 }
 
 // the storage choices of an instance (mpcg_instance_traits): lane parts per stage, row slots
-// per lane, stored 1/t, LEAN / GFH storage, constant [B A] rows, paired chains, LDS bytes
+// per lane, stored 1/t, LEAN / GFH storage, constant [B A] rows, paired chains, LDS bytes, the
+// stage strides (doubles) of the h-row gradients, the h-row gaps and the cost-to-go rows
 template <class C>
 const char* instance_traits() {
     static char buf[192];
-    snprintf(buf, sizeof buf, "parts=%d slots=%d store_it=%d lean=%d gfh=%d fconst=%d pair=%d lds=%d", C::PARTS,
+    using L = LdsOf<C>;
+    snprintf(buf, sizeof buf,
+             "parts=%d slots=%d store_it=%d lean=%d gfh=%d fconst=%d pair=%d lds=%d strides=%d,%d,%d", C::PARTS,
              C::SLOTS, (int)C::STORE_IT, (int)lds_lean<C>(), (int)lds_gfh<C>(), (int)C::FCONST, (int)C::PAIR_CHAINS,
-             (int)sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>()>));
+             (int)sizeof(L), L::DGS, L::HDS, L::PS);
     return buf;
 }
 

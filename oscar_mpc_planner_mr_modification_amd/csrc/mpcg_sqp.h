@@ -40,6 +40,43 @@ __host__ __device__ constexpr int sym(int i, int j) { return i >= j ? i * (i + 1
 // column-major packed lower triangle of an n x n block, a >= c
 __host__ __device__ constexpr int cpk(int n, int a, int c) { return c * n - c * (c - 1) / 2 + (a - c); }
 
+// LDS cycles of one ds_read_b64 in which lane l = k * parts + p reads the double at
+// s * k + off * p (a per-stage array, stage stride s doubles, part offset off): each 32-lane
+// half is one group, dword d sits on bank d mod 64, every extra distinct dword on a busy
+// bank costs a cycle (MI355X_MICROARCH.md §LDS).  Conflict-free = 2.
+__host__ __device__ constexpr int lds_b64_cycles(int s, int off, int parts) {
+    int total = 0;
+    for (int half = 0; half < 2; ++half) {
+        int dw[64] = {};
+        int n = 0;
+        for (int l = 32 * half; l < 32 * half + 32; ++l) {
+            const int a = 2 * (s * (l / parts) + off * (l % parts));
+            for (int h = 0; h < 2; ++h) {
+                bool seen = false;
+                for (int i = 0; i < n; ++i) seen = seen || dw[i] == a + h;
+                if (!seen) dw[n++] = a + h;
+            }
+        }
+        int worst = 0;
+        for (int b = 0; b < 64; ++b) {
+            int c = 0;
+            for (int i = 0; i < n; ++i) c += (dw[i] % 64) == b;
+            worst = c > worst ? c : worst;
+        }
+        total += worst;
+    }
+    return total;
+}
+// the stage stride in [base, base + maxpad] (steps of step) with the fewest such cycles
+__host__ __device__ constexpr int lds_stride(int base, int off, int parts, int step, int maxpad) {
+    int best = base, bc = lds_b64_cycles(base, off, parts);
+    for (int s = base + step; s <= base + maxpad; s += step) {
+        const int c = lds_b64_cycles(s, off, parts);
+        if (c < bc) { bc = c; best = s; }
+    }
+    return best;
+}
+
 // N: horizon, NL / NE / NS: topology halfspaces, obstacle ellipsoids,
 // scenario (or, C3, decomp) halfspaces per stage, NX_: 5 (unicycle) or 6
 // (unicycle + slack state, or the bicycle), MODEL_: 0 contouring unicycle,
@@ -193,9 +230,21 @@ struct Cfg {
 // the four-solves-per-CU line even with the LEAN storage (C3, C4): at one wave per SIMD a
 // CU with three solves leaves a SIMD idle.  They are written once per linearisation and
 // read by the Riccati step (prefetched a stage ahead) and the vector passes.
-template <class C, bool LEAN = C::COMPACT, bool GFH = false>
+//
+// PAD: the row-owner arrays (h-row gradients and gaps, read by every lane at its own stage
+// and rows) and the cost-to-go rows (read by every lane at its own stage in the vector
+// passes) get the stage strides with the fewest LDS bank conflicts (lds_stride; the
+// cost-to-go rows stay 16-B aligned for the Riccati step's broadcast reads), where the
+// padded footprint stays under the four-solves-per-CU line (lds_pad)
+template <class C, bool LEAN = C::COMPACT, bool GFH = false, bool PAD = false>
 struct Lds {
     static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
+    // (an even gradient row keeps its 16-B alignment: its (x, y) pair is one ds_read_b128; JS with
+    // the odd stride 9 measured 41.65 -> 42.03 ms)
+    static constexpr int DGS =
+        PAD ? lds_stride(C::NHS * C::DGC, C::DGC, C::PARTS, C::DGC % 2 == 0 ? 2 : 1, 3) : C::NHS * C::DGC;
+    static constexpr int HDS = PAD ? lds_stride(C::NHS, 1, C::PARTS, 1, 3) : C::NHS;
+    static constexpr int PS = PAD ? lds_stride(C::NPTP, 0, C::PARTS, C::NPTP == C::NPT ? 1 : 2, 4) : C::NPTP;
     double z[N + 1][NZ];      // NLP iterate [u x]
     double H[GFH ? 1 : N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
     double g[N + 1][NZ];
@@ -213,14 +262,14 @@ struct Lds {
     double piq[N][NX];
     double pin[LEAN ? 1 : N][NX];
     double rdyn[LEAN ? 1 : N][NX];
-    alignas(16) double P[N + 1][C::NPTP];  // Riccati cost-to-go, packed (row padded, C::NPTP)
+    alignas(16) double P[N + 1][PS];  // Riccati cost-to-go, packed (row padded, C::NPTP / PS)
     double Lc[N][C::NLC];     // chol(Muu): off-diagonal l_ij (i > j), then 1/l_ii (nu 2: l00 l10 1/l00 1/l11)
     double Y[N][C::NU][NX];   // L^-1 Mux
     double bx[N + 1][NZ];     // per-variable box-row sums, written by the variable's owner lane;
                               // dead from the Newton gradient to the next residuals: holds the
                               // backward vector chain p_k [N][NX] meanwhile
-    double Dg[N][C::NHS][C::DGC];  // signed h-row gradients on (x, y[, psi]); the slack one is C::slack_coef
-    double hd[N][C::NHS];     // h-row bound gaps (uh - h or h - lh)
+    double Dg[N][DGS];        // signed h-row gradients on (x, y[, psi]) per row ([NHS][DGC]); the slack one is C::slack_coef
+    double hd[N][HDS];        // h-row bound gaps (uh - h or h - lh)
     double disc[C::LIN_PARAMS ? N : 1][4];  // LIN_PARAMS: off cos psi, off sin psi, d/dpsi of both
     double Msc[128];          // factorisation scratch: the stage block (lanes < nz(nz+1)/2) and
                               // dummy targets (64 + lane) of the branch-free stores
@@ -242,6 +291,17 @@ __host__ __device__ constexpr bool lds_gfh() {
     return sizeof(Lds<C, lds_lean<C>(), false>) > LDS_QUARTER && sizeof(Lds<C, lds_lean<C>(), true>) <= LDS_QUARTER;
 #endif
 }
+// conflict-minimal strides where they fit under the line (MPCG_NO_STRIDE_PAD: A/B)
+template <class C>
+__host__ __device__ constexpr bool lds_pad() {
+#ifdef MPCG_NO_STRIDE_PAD
+    return false;
+#else
+    return sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), true>) <= LDS_QUARTER;
+#endif
+}
+template <class C>
+using LdsOf = Lds<C, lds_lean<C>(), lds_gfh<C>(), lds_pad<C>()>;
 // doubles of one solve's global workspace (GFH: [B A] blocks, then the Hessian blocks)
 template <class C>
 __host__ __device__ constexpr size_t gfh_doubles() {
@@ -512,7 +572,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
     constexpr bool LEAN = lds_lean<C>();
     constexpr bool GFH = lds_gfh<C>();
-    __shared__ Lds<C, LEAN, GFH> S;
+    __shared__ LdsOf<C> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
     __shared__ char lds_pad[MPCG_LDS_PAD];
@@ -534,7 +594,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     const int kc = k < N ? k : N - 1;    // clamped stage < N
     const int npar = pr.npar;
     constexpr int LAMS = NX + C::NH;  // multiplier block per stage (include/mpcg.h, mpcg_io)
+#ifdef MPCG_DIAG_PARAMS_OF
+    // diagnostic build only (scripts/param_locality.py): solve sol reads the parameter block of
+    // solve sol % MPCG_DIAG_PARAMS_OF (a batch of identical copies: the cost of the parameter reads'
+    // misses)
+    const double* pbase = io.params + (size_t)(sol % MPCG_DIAG_PARAMS_OF) * N * npar;
+#else
     const double* pbase = io.params + (size_t)sol * N * npar;
+#endif
     const double* pk = pbase + (size_t)kc * npar;
     (void)stamps;
     // the stage blocks [B A] (Fb) and H (Hb): LDS, or this solve's global workspace (GFH)
@@ -582,11 +649,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 return;
             }
             const int he = hh - C::NL;
-            a = S.Dg[k][he][0];
-            b = S.Dg[k][he][1];
+            a = S.Dg[k][he * C::DGC + 0];
+            b = S.Dg[k][he * C::DGC + 1];
             c = a * S.disc[k][2] + b * S.disc[k][3];
         } else {
-            a = S.Dg[k][hh][0]; b = S.Dg[k][hh][1]; c = S.Dg[k][hh][2];
+            a = S.Dg[k][hh * C::DGC + 0]; b = S.Dg[k][hh * C::DGC + 1]; c = S.Dg[k][hh * C::DGC + 2];
         }
     };
     auto rowgap = [&](int hh) -> double {
@@ -695,7 +762,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
             double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
+            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, (double (*)[C::DGC])S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
             STAMP_LAP(10);
             // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
             {

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Register, scratch and LDS use of every sqp_kernel instance (compiler remarks; CPU only).
+#   bash scripts/kernel_resources.sh [extra hipcc flags...]
+# one line per kernel: Cfg<N,NL,NE,NS,NX,MODEL> FULL | VGPR AGPR scratch(B/lane) LDS(B)
+C=oscar_mpc_planner_mr_modification_amd/csrc
+for f in mpcg_inst_tmpc20 mpcg_inst_tmpc30 mpcg_inst_shmpc mpcg_inst_bicycle; do
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -I$C "$@" --cuda-device-only -c $C/$f.hip -o /tmp/kr_$f.o \
+      -Rpass-analysis=kernel-resource-usage 2>&1 |
+    awk '/Function Name: .*sqp_kernel/ {n=$0; sub(/.*CfgIL/,"",n); sub(/EEE.*/,"",n); f=($0 ~ /Lb1E/)?"full":"lean";
+                                         gsub(/ELi/,",",n); sub(/^i/,"",n); name="Cfg<" n "> " f; show=1; next}
+         /Function Name:/ {show=0}
+         function num() { match($0, /: [0-9]+/); return substr($0, RSTART + 2, RLENGTH - 2) }
+         show && /VGPRs:/ {v=num()} show && /AGPRs:/ {a=num()} show && /ScratchSize/ {s=num()}
+         show && /LDS Size/ {printf "%-28s VGPR %s AGPR %s scratch %s LDS %s\n", name, v, a, s, num(); show=0}'
+done
