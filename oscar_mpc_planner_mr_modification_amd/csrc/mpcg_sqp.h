@@ -132,11 +132,20 @@ struct Cfg {
     // keeps them out of scratch.  Measured (scripts/ab_bench.py, profiles/r03d_ab_*): JS 42.11 ->
     // 41.39 ms, C5 20.89 -> 20.68, JD unchanged; the stored variant of the two-part instances
     // passed full-size parity (JS, JD: 20,480 solves each, profiles/r03c_variant_storeit.jsonl).
+    // Without it JD and C5 are scratch-free (68 / 28 B/lane with it) but slower: JD 44.47 -> 44.84
+    // ms, C5 20.69 -> 20.91 (profiles/r03k_ab.jsonl, MPCG_STORE_IT_MAX=12).
     // MPCG_STORE_IT_MAX=0 recomputes it everywhere.
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 14
 #endif
     static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
+    // box bounds selected per use instead of held in registers (LaneBounds; MPCG_BOUNDS_SEL=1, A/B
+    // only): C2 went into scratch with it (0 -> 68 B/lane), C3 unchanged, and C4 (148 -> 132 B/lane
+    // of scratch) measured 50.75 vs 50.72 ms in two alternating repetitions (profiles/r03k_ab.jsonl)
+#ifndef MPCG_BOUNDS_SEL
+#define MPCG_BOUNDS_SEL 0
+#endif
+    static constexpr bool BOUNDS_SEL = MPCG_BOUNDS_SEL > 0;
     static constexpr int NBOX = 2 * NU + 2 * NX;  // box rows of a stage in 1..N-1 (input + state bounds)
     // Linear rows (topology and scenario halfspaces) read their coefficients from the
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
@@ -437,17 +446,19 @@ struct Rows {
 
 // The rows of the lane (stage k, part p): box slot j <-> variable v(j) = p + PARTS j,
 // h slot r <-> h row hh(r) = p + PARTS r.
-// MPCG_BOUNDS_SEL: the box bounds of a lane's variables are selected from the uniform problem
+// Cfg::BOUNDS_SEL: the box bounds of a lane's variables are selected from the uniform problem
 // arguments by the lane's part at each use (two v_cndmask per bound) instead of living in
-// 2 BVS VGPR pairs for the whole solve (A/B switch: the register-starved C3 spills them and
-// reloads them in every residual pass)
-#ifndef MPCG_BOUNDS_SEL
-#define MPCG_BOUNDS_SEL 0
-#endif
-template <class C>
-struct LaneRows {
+// 2 BVS VGPR pairs for the whole solve
+template <class C, bool SEL = C::BOUNDS_SEL>
+struct LaneBounds {
     int k, part;
-#if MPCG_BOUNDS_SEL
+    double lo[C::BVS], hi[C::BVS];
+    __device__ __forceinline__ double lo_at(int j) const { return lo[j]; }
+    __device__ __forceinline__ double hi_at(int j) const { return hi[j]; }
+};
+template <class C>
+struct LaneBounds<C, true> {
+    int k, part;
     const mpcg_problem* prb;
     __device__ __forceinline__ static double bnd(const mpcg_problem& p, int v, bool upper) {
         if (v >= C::NZ) return 0.0;
@@ -461,11 +472,11 @@ struct LaneRows {
     }
     __device__ __forceinline__ double lo_at(int j) const { return sel(j, false); }
     __device__ __forceinline__ double hi_at(int j) const { return sel(j, true); }
-#else
-    double lo[C::BVS], hi[C::BVS];
-    __device__ __forceinline__ double lo_at(int j) const { return lo[j]; }
-    __device__ __forceinline__ double hi_at(int j) const { return hi[j]; }
-#endif
+};
+template <class C>
+struct LaneRows : LaneBounds<C> {
+    using LaneBounds<C>::k;
+    using LaneBounds<C>::part;
     __device__ __forceinline__ int var(int j) const { return part + C::PARTS * j; }
     __device__ __forceinline__ int hrow(int r) const { return part + C::PARTS * r; }
     // input bounds on every stage < N, state bounds on 1..N-1
@@ -624,20 +635,20 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     LaneRows<C> LR;
     LR.k = k;
     LR.part = part;
-#if MPCG_BOUNDS_SEL
-    LR.prb = &pr;
-#else
+    if constexpr (C::BOUNDS_SEL) {
+        LR.prb = &pr;
+    } else {
 #pragma unroll
-    for (int j = 0; j < BVS; ++j) {
-        const int v = LR.var(j);
-        double lo = 0.0, hi = 0.0;
+        for (int j = 0; j < BVS; ++j) {
+            const int v = LR.var(j);
+            double lo = 0.0, hi = 0.0;
 #pragma unroll
-        for (int i = 0; i < NZ; ++i)
-            if (v == i) { lo = i < NU ? pr.lbu[i] : pr.lbx[i - NU]; hi = i < NU ? pr.ubu[i] : pr.ubx[i - NU]; }
-        LR.lo[j] = lo;
-        LR.hi[j] = hi;
+            for (int i = 0; i < NZ; ++i)
+                if (v == i) { lo = i < NU ? pr.lbu[i] : pr.lbx[i - NU]; hi = i < NU ? pr.ubu[i] : pr.ubx[i - NU]; }
+            LR.lo[j] = lo;
+            LR.hi[j] = hi;
+        }
     }
-#endif
     // gradient (x, y, psi) and gap of h row hh of this lane's stage
     auto rowg = [&](int hh, double& a, double& b, double& c) {
         if constexpr (C::LIN_PARAMS) {

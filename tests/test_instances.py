@@ -136,3 +136,30 @@ def test_builtin_instances_storage_choices():
     # stored 1/t up to 14 row slots per lane (C1, C2, C5, JS, JD); C3 (16) and C4 (20) recompute it
     for cfg, want in (("C1", "1"), ("C5", "1"), ("JS", "1"), ("JD", "1"), ("C3", "0"), ("C4", "0")):
         assert got[cfg]["store_it"] == want, (cfg, got[cfg])
+    # conflict-minimal LDS stage strides (h-row gradients, h-row gaps, cost-to-go rows; doubles),
+    # every instance still under the four-solves-per-CU line
+    for cfg, want in (("C2", "49,17,18"), ("C1", "25,9,18"), ("C4", "26,14,15"), ("JS", "10,6,15")):
+        assert got[cfg]["strides"] == want, (cfg, got[cfg])
+    for cfg, t in got.items():
+        assert int(t["lds"]) <= 40 * 1024, (cfg, t)
+
+
+def test_lds_stride_model():
+    """The compile-time bank model (mpcg_sqp.h lds_b64_cycles) restated: C2's unpadded
+    h-row gradient rows (48 doubles per stage, part offset 3) cost 12 LDS cycles per
+    ds_read_b64, the padded 49 cost 4; conflict-free is 2."""
+    def cycles(s, off, parts):
+        total = 0
+        for half in range(2):
+            dw = {2 * (s * (lane // parts) + off * (lane % parts)) + h
+                  for lane in range(32 * half, 32 * half + 32) for h in range(2)}
+            per_bank = {}
+            for d in dw:
+                per_bank[d % 64] = per_bank.get(d % 64, 0) + 1
+            total += max(per_bank.values())
+        return total
+    assert cycles(48, 3, 3) == 12 and cycles(49, 3, 3) == 4      # C2 gradients
+    assert cycles(16, 1, 3) == 12 and cycles(17, 1, 3) == 4      # C2 gaps
+    assert cycles(16, 0, 3) == 12 and cycles(18, 0, 3) == 2      # C2 cost-to-go (even strides)
+    assert cycles(24, 2, 2) == 8 and cycles(26, 2, 2) == 4       # C4 gradients (even strides)
+    assert cycles(15, 0, 2) == 2                                  # N 30 cost-to-go, unpadded
