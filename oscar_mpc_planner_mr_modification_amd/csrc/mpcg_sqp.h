@@ -244,8 +244,10 @@ struct Cfg {
 // and rows) and the cost-to-go rows (read by every lane at its own stage in the vector
 // passes) get the stage strides with the fewest LDS bank conflicts (lds_stride; the
 // cost-to-go rows stay 16-B aligned for the Riccati step's broadcast reads), where the
-// padded footprint stays under the four-solves-per-CU line (lds_pad)
-template <class C, bool LEAN = C::COMPACT, bool GFH = false, bool PAD = false>
+// padded footprint stays under the four-solves-per-CU line (lds_pad).  PAD 2 also pads the
+// unpadded odd cost-to-go rows of the long horizons to an even conflict-free stride (16-B
+// aligned broadcast reads; N 30: 15 -> 18 doubles) where that still fits
+template <class C, bool LEAN = C::COMPACT, bool GFH = false, int PAD = 0>
 struct Lds {
     static constexpr int N = C::N, NX = C::NX, NZ = C::NZ;
     // (an even gradient row keeps its 16-B alignment: its (x, y) pair is one ds_read_b128; JS with
@@ -253,7 +255,9 @@ struct Lds {
     static constexpr int DGS =
         PAD ? lds_stride(C::NHS * C::DGC, C::DGC, C::PARTS, C::DGC % 2 == 0 ? 2 : 1, 3) : C::NHS * C::DGC;
     static constexpr int HDS = PAD ? lds_stride(C::NHS, 1, C::PARTS, 1, 3) : C::NHS;
-    static constexpr int PS = PAD ? lds_stride(C::NPTP, 0, C::PARTS, C::NPTP == C::NPT ? 1 : 2, 4) : C::NPTP;
+    static constexpr int PS = PAD == 0   ? C::NPTP
+                              : PAD == 2 ? lds_stride(C::NPT + (C::NPT & 1), 0, C::PARTS, 2, 4)
+                                         : lds_stride(C::NPTP, 0, C::PARTS, C::NPTP == C::NPT ? 1 : 2, 4);
     double z[N + 1][NZ];      // NLP iterate [u x]
     double H[GFH ? 1 : N + 1][C::NHP];  // MIRROR-regularised Lagrangian Hessian, packed lower triangle (C::COMPACT)
     double g[N + 1][NZ];
@@ -302,11 +306,18 @@ __host__ __device__ constexpr bool lds_gfh() {
 }
 // conflict-minimal strides where they fit under the line (MPCG_NO_STRIDE_PAD: A/B)
 template <class C>
-__host__ __device__ constexpr bool lds_pad() {
-#ifdef MPCG_NO_STRIDE_PAD
-    return false;
+__host__ __device__ constexpr int lds_pad() {
+#if defined(MPCG_NO_STRIDE_PAD)
+    return 0;
 #else
-    return sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), true>) <= LDS_QUARTER;
+#if defined(MPCG_NO_P_ALIGN)
+    constexpr bool P_ALIGN = false;
+#else
+    constexpr bool P_ALIGN = true;
+#endif
+    return P_ALIGN && sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), 2>) <= LDS_QUARTER ? 2
+           : sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), 1>) <= LDS_QUARTER         ? 1
+                                                                                   : 0;
 #endif
 }
 template <class C>
@@ -1281,6 +1292,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     double fi[NX], fj[NX], hv;
 #pragma unroll
                     for (int m = 0; m < NX; ++m) { fi[m] = Fat(N - 1, m, ei); fj[m] = Fat(N - 1, m, ej); }
+                    // rows of [B A] that vary over the stages: with the constant rows (FCONST) only x+ and
+                    // y+; the others stay in fi / fj from the fill above (their per-stage re-evaluation
+                    // on the lane's runtime column compiled to branches inside the recursion)
+                    constexpr int NFV = C::FCONST ? C::NFR : NX;
                     // packed Hessian entry of the element lane (the compact storage: slack row / column 0
                     // but the diagonal)
                     auto Hel = [&](int kq) -> double {
@@ -1333,11 +1348,11 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         auto prefetch = [&]() {
                             if constexpr (STG) {
 #pragma unroll
-                                for (int m = 0; m < NX; ++m) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
+                                for (int m = 0; m < NFV; ++m) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
                                 hv2 = HelS() + S.dH[kn][dhd] + S.dH[kn][dhb];
                             } else {
 #pragma unroll
-                                for (int m = 0; m < NX; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
+                                for (int m = 0; m < NFV; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
                                 hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
                             }
                         };
@@ -1468,7 +1483,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             }
                         }
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
+                        for (int m = 0; m < NFV; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
                         hv = hv2;
                         STAMP_LAP(18);
                         wave_sync();
