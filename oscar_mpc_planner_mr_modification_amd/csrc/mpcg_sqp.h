@@ -313,7 +313,7 @@ __host__ __device__ constexpr int lds_pad() {
 #if defined(MPCG_NO_P_ALIGN)
     constexpr bool P_ALIGN = false;
 #else
-    constexpr bool P_ALIGN = true;
+    constexpr bool P_ALIGN = !C::COMPACT;  // C3 with 21 -> 22: 21.14 -> 21.40 ms (profiles/r03n_ab.jsonl)
 #endif
     return P_ALIGN && sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), 2>) <= LDS_QUARTER ? 2
            : sizeof(Lds<C, lds_lean<C>(), lds_gfh<C>(), 1>) <= LDS_QUARTER         ? 1
@@ -1296,6 +1296,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     // y+; the others stay in fi / fj from the fill above (their per-stage re-evaluation
                     // on the lane's runtime column compiled to branches inside the recursion)
                     constexpr int NFV = C::FCONST ? C::NFR : NX;
+                    // (the compact bicycle storage: its v+ and delta+ rows are the known constants)
+                    auto varies = [](int m) { return !C::COMPACT || (m != 3 && m != 4); };
                     // packed Hessian entry of the element lane (the compact storage: slack row / column 0
                     // but the diagonal)
                     auto Hel = [&](int kq) -> double {
@@ -1348,11 +1350,13 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         auto prefetch = [&]() {
                             if constexpr (STG) {
 #pragma unroll
-                                for (int m = 0; m < NFV; ++m) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
+                                for (int m = 0; m < NFV; ++m)
+                                    if (varies(m)) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
                                 hv2 = HelS() + S.dH[kn][dhd] + S.dH[kn][dhb];
                             } else {
 #pragma unroll
-                                for (int m = 0; m < NFV; ++m) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
+                                for (int m = 0; m < NFV; ++m)
+                                    if (varies(m)) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
                                 hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
                             }
                         };
@@ -1483,7 +1487,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             }
                         }
 #pragma unroll
-                        for (int m = 0; m < NFV; ++m) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
+                        for (int m = 0; m < NFV; ++m)
+                            if (varies(m)) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
                         hv = hv2;
                         STAMP_LAP(18);
                         wave_sync();
