@@ -1164,9 +1164,16 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     }
                 }
             }
+#ifdef MPCG_TRACE
             rs = wave_max(rs);
             re = wave_max(re);
             ri = wave_max(ri);
+#else
+            // the exit tests compare all three residuals with the same bounds: one reduction of
+            // their lane maximum (fmax drops NaN exactly as the per-lane accumulation above does)
+            rs = wave_max(fmax(fmax(rs, re), ri));
+            re = ri = rs;
+#endif
             comp = wave_sum(comp);
             const double mu = comp / C::M_TOTAL;
 #ifdef MPCG_TRACE
