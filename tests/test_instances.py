@@ -138,7 +138,7 @@ def test_builtin_instances_storage_choices():
         assert got[cfg]["store_it"] == want, (cfg, got[cfg])
     # conflict-minimal LDS stage strides (h-row gradients, h-row gaps, cost-to-go rows; doubles),
     # every instance still under the four-solves-per-CU line
-    for cfg, want in (("C2", "49,17,18"), ("C1", "25,9,18"), ("C4", "26,14,15"), ("JS", "10,6,15")):
+    for cfg, want in (("C2", "49,17,18"), ("C1", "25,9,18"), ("C4", "26,14,18"), ("JS", "10,6,15")):
         assert got[cfg]["strides"] == want, (cfg, got[cfg])
     for cfg, t in got.items():
         assert int(t["lds"]) <= 40 * 1024, (cfg, t)
