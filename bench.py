@@ -212,7 +212,6 @@ class TmpcWorkload(Workload):
 
     def step(self, ev=None):
         from oscar_mpc_planner_mr_modification_amd import native
-        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
         from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION, ROBOT_RADIUS, SETTINGS_WEIGHTS
 
         s = self.stream
@@ -232,7 +231,8 @@ class TmpcWorkload(Workload):
                                             consistency_enabled=self.prep["consistency_active"],
                                             previously_selected=self.dsc["previously_selected"],
                                             selection_weight=0.75, stream=s)   # guidance_planner.yaml:37
-        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, self.G, out=self.winners)
+        native.winner_records_device(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, self.G, self.winners,
+                                     stream=s)
         self.gather(self.winners)
 
     def host_inputs(self, lo, hi):
@@ -277,7 +277,6 @@ class C3Workload(Workload):
         import torch
 
         from oscar_mpc_planner_mr_modification_amd import native
-        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
 
         s = self.stream
         if ev:
@@ -286,7 +285,7 @@ class C3Workload(Workload):
         if ev:
             ev[1].record(s)
         best = torch.where(self.out["exit"] == 1, 0, -1).to(torch.int32)
-        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, 1, out=self.winners)
+        native.winner_records_device(self.out["xtraj"], self.out["utraj"], self.out["pobj"], best, 1, self.winners, stream=s)
         self.gather(self.winners)
 
     def host_inputs(self, lo, hi):
@@ -351,7 +350,6 @@ class ShmpcWorkload(Workload):
 
     def step(self, ev=None):
         from oscar_mpc_planner_mr_modification_amd import native
-        from oscar_mpc_planner_mr_modification_amd.distributed import winner_records
         from oscar_mpc_planner_mr_modification_amd.synthetic import DECELERATION
 
         s = self.stream
@@ -366,7 +364,8 @@ class ShmpcWorkload(Workload):
         if ev:
             ev[2].record(s)
         native.select_lowest_cost_device(self.S, self.P, self.out["pobj"], self.out["exit"], out=self.best, stream=s)
-        winner_records(self.out["xtraj"], self.out["utraj"], self.out["pobj"], self.best, self.P, out=self.winners)
+        native.winner_records_device(self.out["xtraj"], self.out["utraj"], self.out["pobj"], self.best, self.P,
+                                     self.winners, stream=s)
         self.gather(self.winners)
 
     def host_inputs(self, lo, hi):

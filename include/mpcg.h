@@ -350,6 +350,15 @@ int mpcg_select_best_device(int n_scenes, int n_guesses, int N,
                             const unsigned char *disabled,
                             int *best, double *objective, void *stream);
 
+/* Per-scene record of the selected planner for the winner all-gather (the device form of
+ * distributed.winner_records; the reference hands the winner's trajectory to the module,
+ * guidance_constraints.cpp:429-442): out[n_scenes][(N+1)*nx + N*nu + 2] =
+ * xtraj | utraj | pobj | best of planner max(best, 0) (best == -1: planner 0, index -1 kept).
+ * xtraj [n_scenes*G][N+1][nx], utraj [..][N][nu], pobj [..], best [n_scenes].  Device pointers. */
+int mpcg_winner_records_device(int n_scenes, int n_guesses, int N, int nx, int nu,
+                               const double *xtraj, const double *utraj, const double *pobj,
+                               const int *best, double *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

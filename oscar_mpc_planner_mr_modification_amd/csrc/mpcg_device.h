@@ -390,6 +390,19 @@ __device__ inline void erk_unicycle(const mpcg_problem& pr, const double z[NU + 
 // the convergence test exactly as in the full-size sweep)
 // NA: the leading NA x NA block of the NZ x NZ array is mirrored in place
 // (NA < NZ: the trailing rows / columns are decoupled and handled by the caller)
+// MPCG_MIRROR_RR=1: the round-robin (parallel) Jacobi ordering below, A/B only -- measured slower
+// (profiles/r03q_ab.jsonl: C2 11.97 -> 12.04 ms, C1 +1.6 %, C5 +1.3 %, JS +1.2 %; C4 -1.0 %) and its
+// different rounding moved one C5 copy of 8,192 to another exit (1602: QP failure in the oracle,
+// success on the GPU; profiles/r03q_rr_fullsize.log)
+#ifndef MPCG_MIRROR_RR
+#define MPCG_MIRROR_RR 0
+#endif
+// round-robin schedule of n (even) players: pair i of round r (players n - 1 and r, then
+// (r + i, r - i) mod n - 1), lower / higher index
+__host__ __device__ constexpr int rr_a(int n, int r, int i) { return i == 0 ? n - 1 : (r + i) % (n - 1); }
+__host__ __device__ constexpr int rr_b(int n, int r, int i) { return i == 0 ? r : (r - i + n - 1) % (n - 1); }
+__host__ __device__ constexpr int rr_lo(int n, int r, int i) { return rr_a(n, r, i) < rr_b(n, r, i) ? rr_a(n, r, i) : rr_b(n, r, i); }
+__host__ __device__ constexpr int rr_hi(int n, int r, int i) { return rr_a(n, r, i) < rr_b(n, r, i) ? rr_b(n, r, i) : rr_a(n, r, i); }
 template <int NZ, int NA = NZ>
 __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0.0) {
     // Cyclic Jacobi on the symmetric part, one-sided rotation updates on the
@@ -414,6 +427,58 @@ __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0
             for (int j = i + 1; j < NA; ++j) off += A[i][j] * A[i][j];
         }
         if (off <= 1e-32 * dia || off < 1e-300) break;
+#if MPCG_MIRROR_RR
+        // round-robin (parallel) ordering: the pairs of a round are disjoint, so their rotation
+        // parameters depend only on the round's starting entries and their reciprocal / square
+        // root chains run side by side; the rotations are then applied one after the other
+        constexpr int NPL = NA + (NA & 1), NPR = NPL / 2;
+#pragma unroll
+        for (int rd = 0; rd < NPL - 1; ++rd) {
+            double tr[NPR], snr[NPR], taur[NPR];
+            bool on[NPR];
+#pragma unroll
+            for (int i = 0; i < NPR; ++i) {
+                const int p = rr_lo(NPL, rd, i), q = rr_hi(NPL, rd, i);
+                on[i] = false;
+                if (q >= NA) continue;  // the bye of an odd count
+                const double apq = A[p][q];
+                on[i] = fabs(apq) >= 1e-300;
+                const double theta = 0.5 * (A[q][q] - A[p][p]) * frcp(on[i] ? apq : 1.0);
+                const double at = fabs(theta);
+                double t = at < 1e150 ? frcp(at + fsqrt_pos(fma(at, at, 1.0))) : 0.5 * frcp(at);
+                t = theta >= 0.0 ? t : -t;
+                const double c = frsq(fma(t, t, 1.0));
+                tr[i] = t;
+                snr[i] = t * c;
+                taur[i] = snr[i] * frcp(1.0 + c);
+            }
+#pragma unroll
+            for (int i = 0; i < NPR; ++i) {
+                const int p = rr_lo(NPL, rd, i), q = rr_hi(NPL, rd, i);
+                if (q >= NA || !on[i]) continue;
+                const double apq = A[p][q], t = tr[i], sn = snr[i], tau = taur[i];
+                A[p][p] -= t * apq;
+                A[q][q] += t * apq;
+                A[p][q] = 0.0;
+#pragma unroll
+                for (int r = 0; r < NA; ++r) {
+                    if (r == p || r == q) continue;
+                    double& arp = r < p ? A[r][p] : A[p][r];
+                    double& arq = r < q ? A[r][q] : A[q][r];
+                    const double g = arp, h = arq;
+                    arp = g - sn * fma(g, tau, h);
+                    arq = h + sn * fma(-h, tau, g);
+                }
+#pragma unroll
+                for (int r = 0; r < NA; ++r) {
+                    const double g = V[r][p], h = V[r][q];
+                    V[r][p] = g - sn * fma(g, tau, h);
+                    V[r][q] = h + sn * fma(-h, tau, g);
+                }
+            }
+        }
+        continue;
+#endif
 #pragma unroll
         for (int p = 0; p < NA - 1; ++p)
 #pragma unroll

@@ -61,6 +61,27 @@ __global__ void select_best_kernel(int n_scenes, int G, int N, const double* __r
     best[sc] = best_i;
 }
 
+// ---- per-scene record of the selected planner: xtraj | utraj | pobj | index (best -1 records
+// planner 0, whose exit code the reference returns then, guidance_constraints.cpp:429-442); one
+// wave per scene, coalesced copies
+__global__ void winner_records_kernel(int G, int N, int nx, int nu, const double* __restrict__ xtraj,
+                                      const double* __restrict__ utraj, const double* __restrict__ pobj,
+                                      const int* __restrict__ best, double* __restrict__ out) {
+    const int sc = blockIdx.x;
+    const int nxt = (N + 1) * nx, nut = N * nu, w = nxt + nut + 2;
+    const int b = best[sc];
+    const size_t s = (size_t)sc * G + (b < 0 ? 0 : b);
+    double* o = out + (size_t)sc * w;
+    for (int e = threadIdx.x; e < w; e += blockDim.x) {
+        double v;
+        if (e < nxt) v = xtraj[s * nxt + e];
+        else if (e < nxt + nut) v = utraj[s * nut + (e - nxt)];
+        else if (e == nxt + nut) v = pobj[s];
+        else v = (double)b;
+        o[e] = v;
+    }
+}
+
 // ---- ScenarioConstraints::optimize's pick (scenario_constraints.cpp:86-103)
 __global__ void select_lowest_cost_kernel(int n_scenes, int P, const double* __restrict__ pobj,
                                           const int* __restrict__ exit_code, int* __restrict__ best) {
@@ -564,6 +585,24 @@ int mpcg_select_best_device(int n_scenes, int n_guesses, int N, const double* xt
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         mpcg::g_err = std::string("select_best launch: ") + hipGetErrorString(e);
+        return -1;
+    }
+    return 0;
+}
+
+int mpcg_winner_records_device(int n_scenes, int n_guesses, int N, int nx, int nu, const double* xtraj,
+                               const double* utraj, const double* pobj, const int* best, double* out, void* stream) {
+    if (n_scenes < 0 || n_guesses < 1 || N < 1 || nx < 1 || nu < 1 ||
+        (n_scenes > 0 && (!xtraj || !utraj || !pobj || !best || !out))) {
+        mpcg::g_err = "mpcg_winner_records_device: invalid arguments";
+        return -1;
+    }
+    if (n_scenes == 0) return 0;
+    hipLaunchKernelGGL(mpcg::winner_records_kernel, dim3(n_scenes), dim3(64), 0, (hipStream_t)stream, n_guesses, N, nx,
+                       nu, xtraj, utraj, pobj, best, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        mpcg::g_err = std::string("winner_records launch: ") + hipGetErrorString(e);
         return -1;
     }
     return 0;

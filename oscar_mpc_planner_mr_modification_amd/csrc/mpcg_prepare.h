@@ -58,7 +58,6 @@ __device__ __forceinline__ void dr_reflect(double px, double py, double cx, doub
 
 struct PrepLds {
     double warm[PREP_MAX_N + 1][MPCG_NVAR];
-    double lin[PREP_MAX_N][PREP_MAX_OBS][3];
     double prev[PREP_MAX_N][2];
     int prev_ok;
 };
@@ -154,15 +153,18 @@ __global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scen
                 px = __dmul_rn(0.5, __dadd_rn(px, rx));
                 py = __dmul_rn(0.5, __dadd_rn(py, ry));
             }
+        // straight into the stage's parameter row (the stream below skips these entries): no
+        // [N][obstacles] staging array in LDS, whose 18 KB held the kernel at 7 workgroups per CU
+        double* Pl = params + ((size_t)sol * N + k) * npar + pr.i_lin0;
         for (int i = 0; i < n_obs; ++i) {
             double ox, oy;
             opos(i, ox, oy);
             const double dx = __dsub_rn(ox, px), dy = __dsub_rn(oy, py);
             const double dist = norm2_rn(dx, dy);
             const double a1 = __ddiv_rn(dx, dist), a2 = __ddiv_rn(dy, dist);
-            L.lin[k][i][0] = a1;
-            L.lin[k][i][1] = a2;
-            L.lin[k][i][2] = __dsub_rn(__dadd_rn(__dmul_rn(a1, ox), __dmul_rn(a2, oy)), rr);
+            Pl[3 * i + 0] = a1;
+            Pl[3 * i + 1] = a2;
+            Pl[3 * i + 2] = __dsub_rn(__dadd_rn(__dmul_rn(a1, ox), __dmul_rn(a2, oy)), rr);
         }
     }
     // ---- previous plan interpolated by the elapsed time
@@ -209,13 +211,18 @@ __global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scen
     const double* base = in.stage_params + (size_t)sc * npar;
     double* P = params + (size_t)sol * N * npar;
     const int lin0 = pr.i_lin0, ell0 = pr.i_ell0;
+    // (stage, index) of element e = lane + 64 it, advanced without a division per element
+    int k = lane / npar, idx = lane - (lane / npar) * npar;
     for (int e = lane; e < N * npar; e += 64) {
-        const int k = e / npar, idx = e - k * npar;
+        if (e > lane) {
+            idx += 64;
+            while (idx >= npar) { idx -= npar; ++k; }
+        }
         double v = base[idx];
         if (NL > 0 && idx >= lin0 && idx < lin0 + 3 * NL) {
             const int i = (idx - lin0) / 3, c = (idx - lin0) - 3 * i;
-            if (guided && k >= 1 && i < n_obs) v = L.lin[k][i][c];
-            else v = c == 0 ? 1.0 : (c == 1 ? 0.0 : __dadd_rn(x0, 100.0));
+            if (guided && k >= 1 && i < n_obs) continue;  // written by the stage's DR lane
+            v = c == 0 ? 1.0 : (c == 1 ? 0.0 : __dadd_rn(x0, 100.0));
         } else if (NE > 0 && idx >= ell0 && idx < ell0 + 7 * NE) {
             const int j = (idx - ell0) / 7, c = (idx - ell0) - 7 * j;
             if (k == 0) {

@@ -182,7 +182,13 @@ struct Cfg {
     // rows shrink the per-solve block 15.3 -> 10.3 KB: 52.85 -> 51.26 ms, 304.5k -> 314.0k solves/s
     // (profiles/r02v_ab_*_C4.json; at three solves per CU, before GFH, it was 2.6 % slower).  On
     // N 20 the constant rows changed the register allocation into scratch (C2 0 -> 128 B/lane).
-    static constexpr bool FCONST = MODEL_ == 0 && N_ >= 30;
+    // (MPCG_FCONST_N=20, A/B: the N 20 instances with the constant rows and their hoisting went into
+    // scratch and ran slower -- C2 11.97 -> 13.34 ms, C5 19.46 -> 25.71, C1 10.43 -> 11.21;
+    // profiles/r03q_ab.jsonl)
+#ifndef MPCG_FCONST_N
+#define MPCG_FCONST_N 30
+#endif
+    static constexpr bool FCONST = MODEL_ == 0 && N_ >= MPCG_FCONST_N;
     static constexpr int NFR = COMPACT ? 4 : (FCONST ? 2 : NX), NFC = COMPACT ? NZ - 1 : NZ;
     static constexpr int NHP = COMPACT ? (NZ - 1) * NZ / 2 + 1 : NTRI;
     // the vector chains split over the parts of a stage (rows of the backward map, columns of
@@ -594,6 +600,29 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
     constexpr bool LEAN = lds_lean<C>();
     constexpr bool GFH = lds_gfh<C>();
+    // the predictor's barrier pass fused into the residual pass: its barrier terms come from the row
+    // state the residual pass has just computed, with the same operations, and one box-sum exchange,
+    // loop and fold fewer per interior-point iteration (wasted only on the iteration that exits).
+    // Measured (profiles/r03q_ab.jsonl, two alternating repetitions): C2 12.32 -> 11.97 ms, C1 10.61
+    // -> 10.43, C4 47.48 -> 45.38, C5 20.60 -> 19.46, JS 38.32 -> 37.17.  (MPCG_FUSE_BAR=0: A/B)
+#ifndef MPCG_FUSE_BAR
+#define MPCG_FUSE_BAR 1
+#endif
+    constexpr bool FUSE_BAR = MPCG_FUSE_BAR > 0;
+    // RES_SPLIT: the stage algebra of the residual and barrier passes (H dz, the stationarity rows,
+    // the Newton gradient, the dynamics rows) split over the parts of a stage -- part p owns the
+    // rows of its box variables p, p + PARTS, ... (and dynamics rows p, p + PARTS, ...), whose box
+    // sums it holds in registers -- instead of one stage lane doing all of them while the other
+    // parts wait.  Same operations per row.  Measured (profiles/r03r_ab.jsonl, two alternating
+    // repetitions): C2 11.99 -> 11.68 ms, C1 10.42 -> 10.15, C5 unchanged; on the two-part long
+    // horizons it moves the allocation into scratch (C4 45.29 -> 46.76, JD 40.45 -> 40.70, JS
+    // 37.25 -> 37.13), so three-part instances only.  (MPCG_RES_SPLIT=0: off, 2: every instance)
+#ifndef MPCG_RES_SPLIT
+#define MPCG_RES_SPLIT 1
+#endif
+    constexpr bool RES_SPLIT = MPCG_RES_SPLIT > 0 && FUSE_BAR && !C::COMPACT && PARTS > 1 && 2 * NB <= NZ &&
+                               (PARTS == 3 || MPCG_RES_SPLIT > 1);
+    constexpr int DRS = (NX + PARTS - 1) / PARTS;  // dynamics rows per part
     __shared__ LdsOf<C> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
@@ -1057,7 +1086,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
         STAMP_END(1);
         int qstat = AC_MAXITER, qit = 0;
         double pinr[LEAN ? NX : 1];  // LEAN: the new dynamics multipliers of the own stage
-        double Hdz[NZ];  // part 0: H_k dz_k of the current iterate
+        double Hdz[RES_SPLIT ? BVS : NZ];  // H_k dz_k of the current iterate: part 0 (RES_SPLIT: the lane's variables)
         for (;; ++qit) {
             if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
             // ---- residuals
@@ -1067,9 +1096,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 double zk[NZ], dzk[NZ];
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) { dzk[i] = S.dz[ks][i]; zk[i] = S.z[ks][i]; }
-                double rh[NB];
+                double rh[NB], qh[NB], dbh[NBT], rbj[BVS], qbj[BVS];
 #pragma unroll
-                for (int i = 0; i < NB; ++i) rh[i] = 0.0;
+                for (int i = 0; i < NB; ++i) rh[i] = qh[i] = 0.0;
+#pragma unroll
+                for (int i = 0; i < NBT; ++i) dbh[i] = 0.0;
+                // FUSE_BAR: the predictor's barrier terms (rc = l t, the same operations as the
+                // barrier pass) from the row state just computed
+                auto bar0 = [&](int s, double& coef, double& wgt) {
+                    const double l = R.l[s], t = R.t[s], itt = R.it(s);
+                    const double rc = l * t;
+                    coef = l + (l * R.rin[s] - rc) * itt;
+                    wgt = l * itt;
+                };
                 auto row_res = [&](int s, double ddot, double gap) {
                     const double l = R.l[s], t = R.t[s];
                     const double rin = ddot + t - gap;
@@ -1080,19 +1119,35 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 };
 #pragma unroll
                 for (int j = 0; j < BVS; ++j) {
-                    double rb = 0.0;
+                    double& rb = rbj[j];
+                    double& qb = qbj[j];
+                    double dd = 0.0;
+                    rb = qb = 0.0;
                     if (LR.box_on(j)) {
                         const int v = LR.var(j);
                         const double zv = S.z[k][v], dzv = S.dz[k][v];
                         rb = R.l[2 * j + 1] - R.l[2 * j];
                         row_res(2 * j, -dzv, zv - LR.lo_at(j));
                         row_res(2 * j + 1, dzv, LR.hi_at(j) - zv);
+                        if constexpr (FUSE_BAR) {
+                            double c0, w0, c1, w1;
+                            bar0(2 * j, c0, w0);
+                            bar0(2 * j + 1, c1, w1);
+                            qb = c1 - c0;
+                            dd = w0 + w1;
+                        }
                     } else {
                         R.rin[2 * j] = R.rin[2 * j + 1] = 0.0;
                         R.set_it(2 * j, 1.0);
                         R.set_it(2 * j + 1, 1.0);
                     }
-                    if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = rb;
+                    if (k <= N && LR.var(j) < NZ) {
+                        if constexpr (!RES_SPLIT) S.bx[k][LR.var(j)] = rb;
+                        if constexpr (FUSE_BAR) {
+                            if constexpr (!RES_SPLIT) S.q[k][LR.var(j)] = qb;  // dead since the last vector pass
+                            S.dH[k][LR.var(j)] = dd;
+                        }
+                    }
                 }
 #pragma unroll
                 for (int r = 0; r < HS; ++r) {
@@ -1113,14 +1168,89 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         dd += sc * dzk[ZS];
                     }
                     row_res(HB + r, dd, rowgap(hh));
+                    if constexpr (FUSE_BAR) {
+                        double coef, wgt;
+                        bar0(HB + r, coef, wgt);
+                        double dg[NB];
+                        dg[0] = a; dg[1] = bq; dg[2] = c;
+                        if constexpr (NB == 4) dg[3] = C::slack_coef(hh);
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) qh[i] += dg[i] * coef;
+#pragma unroll
+                        for (int cc = 0; cc < NB; ++cc)
+#pragma unroll
+                            for (int aa = cc; aa < NB; ++aa) dbh[cpk(NB, aa, cc)] += dg[aa] * wgt * dg[cc];
+                    }
                 }
-                double acc[NB];
+                double acc[NB], aq[NB], ab[NBT];
 #pragma unroll
-                for (int i = 0; i < NB; ++i) acc[i] = rh[i];
+                for (int i = 0; i < NB; ++i) { acc[i] = rh[i]; aq[i] = qh[i]; }
 #pragma unroll
-                for (int p = 1; p < PARTS; ++p)
+                for (int i = 0; i < NBT; ++i) ab[i] = dbh[i];
+#pragma unroll
+                for (int p = 1; p < PARTS; ++p) {
 #pragma unroll
                     for (int i = 0; i < NB; ++i) acc[i] += lane_down(rh[i], p);
+                    if constexpr (FUSE_BAR) {
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) aq[i] += lane_down(qh[i], p);
+#pragma unroll
+                        for (int i = 0; i < NBT; ++i) ab[i] += lane_down(dbh[i], p);
+                    }
+                }
+                if constexpr (RES_SPLIT) {
+                    // part 0's stage sums of the h rows to the owners of the block variables
+                    if (stage_lane) {
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) { S.bx[k][i] = acc[i]; S.bx[k][NB + i] = aq[i]; }
+#pragma unroll
+                        for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
+                    }
+                    wave_sync();
+                    if (k <= N) {
+                        double pq[NX];
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) pq[m] = k < N ? S.piq[k][m] : 0.0;
+#pragma unroll
+                        for (int j = 0; j < BVS; ++j) {
+                            const int v = LR.var(j);
+                            if (v >= NZ) continue;
+                            double a = 0.0;
+#pragma unroll
+                            for (int jj = 0; jj < NZ; ++jj) a += Hat(k, v, jj) * dzk[jj];
+                            Hdz[j] = a;
+                            const int bi = C::blk(v);
+                            double rbox = rbj[j];
+                            if (bi >= 0) rbox += S.bx[k][bi];
+                            double rr = a + S.g[k][v] + rbox;
+                            {
+                                // the predictor's Newton gradient (barrier pass)
+                                double qv = a + S.g[k][v] + qbj[j];
+                                if (bi >= 0) qv += S.bx[k][NB + bi];
+                                S.q[k][v] = qv;
+                            }
+                            if (k < N) {
+#pragma unroll
+                                for (int m = 0; m < NX; ++m) rr += Fat(k, m, v) * pq[m];
+                            }
+                            if (k > 0 && v >= NU) rr -= S.piq[k - 1][v - NU];
+                            const bool free_var = (k == N) ? (v >= NU) : ((k == 0) ? (v < NU) : true);
+                            if (free_var) rs = fmax(rs, fabs(rr));
+                        }
+                        if (k < N) {
+#pragma unroll
+                            for (int jd = 0; jd < DRS; ++jd) {
+                                const int i = part + PARTS * jd;
+                                if (i >= NX) continue;
+                                double a = S.b[k][i] - S.dz[k + 1][NU + i];
+#pragma unroll
+                                for (int jj = 0; jj < NZ; ++jj) a += Fat(k, i, jj) * dzk[jj];
+                                if constexpr (!LEAN) S.rdyn[k][i] = a;
+                                re = fmax(re, fabs(a));
+                            }
+                        }
+                    }
+                } else {
                 wave_sync();  // the owner lanes' box sums S.bx
                 if (stage_lane) {
                     double rbox[NZ];
@@ -1134,8 +1264,17 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         double a = 0.0;
 #pragma unroll
                         for (int j = 0; j < NZ; ++j) a += Hat(k, i, j) * dzk[j];
-                        Hdz[i] = a;
+                        if constexpr (!RES_SPLIT) Hdz[i] = a;
                         r[i] = a + S.g[k][i] + rbox[i];
+                    }
+                    if constexpr (FUSE_BAR) {
+                        // the predictor's Newton gradient and h-row barrier block (barrier pass)
+#pragma unroll
+                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[RES_SPLIT ? 0 : i] + S.g[k][i] + S.q[k][i];
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) S.q[k][C::bvar(i)] += aq[i];
+#pragma unroll
+                        for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
                     }
                     if (k < N) {
 #pragma unroll
@@ -1162,6 +1301,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
                         if (free_var) rs = fmax(rs, fabs(r[i]));
                     }
+                }
                 }
             }
 #ifdef MPCG_TRACE
@@ -1190,9 +1330,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 
             double alpha = 1.0, sigma_mu = 0.0;
             for (int phase = 0; phase < 2; ++phase) {
-                // ---- barrier terms + Newton gradient
+                // ---- barrier terms + Newton gradient (FUSE_BAR: the predictor's came with the residuals)
                 STAMP_BEGIN();
-                {
+                if (!FUSE_BAR || phase == 1) {
                     double qh[NB], dbh[NBT];
 #pragma unroll
                     for (int i = 0; i < NB; ++i) qh[i] = 0.0;
@@ -1205,6 +1345,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         coef = l + (l * R.rin[s] - rc) * itt;
                         wgt = l * itt;
                     };
+                    double qbj[BVS];
 #pragma unroll
                     for (int j = 0; j < BVS; ++j) {
                         double qb = 0.0, dd = 0.0;
@@ -1215,8 +1356,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             qb = c1 - c0;
                             dd = w0 + w1;
                         }
+                        qbj[j] = qb;
                         if (k <= N && LR.var(j) < NZ) {
-                            S.bx[k][LR.var(j)] = qb;
+                            if constexpr (!RES_SPLIT) S.bx[k][LR.var(j)] = qb;
                             if (phase == 0) S.dH[k][LR.var(j)] = dd;
                         }
                     }
@@ -1252,10 +1394,30 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int i = 0; i < NBT; ++i) ab[i] += lane_down(dbh[i], p);
                         }
                     }
+                    if constexpr (RES_SPLIT) {
+                        // part 0's h-row sums to the owners of the block variables, then every
+                        // owner its variables' entries of the Newton gradient
+                        if (stage_lane) {
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) S.bx[k][i] = aq[i];
+                        }
+                        wave_sync();
+                        if (k <= N) {
+#pragma unroll
+                            for (int j = 0; j < BVS; ++j) {
+                                const int v = LR.var(j);
+                                if (v >= NZ) continue;
+                                const int bi = C::blk(v);
+                                double qv = Hdz[j] + S.g[k][v] + qbj[j];
+                                if (bi >= 0) qv += S.bx[k][bi];
+                                S.q[k][v] = qv;
+                            }
+                        }
+                    } else {
                     wave_sync();  // the owner lanes' box sums S.bx
                     if (stage_lane) {
 #pragma unroll
-                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[i] + S.g[k][i] + S.bx[k][i];
+                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[RES_SPLIT ? 0 : i] + S.g[k][i] + S.bx[k][i];
 #pragma unroll
                         for (int i = 0; i < NB; ++i) S.q[k][C::bvar(i)] += aq[i];
                         if (phase == 0) {
@@ -1263,8 +1425,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                             for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
                         }
                     }
+                    }
+                    wave_sync();
                 }
-                wave_sync();
                 STAMP_END(3);
                 // ---- Riccati factorisation (predictor only; the corrector reuses it)
                 STAMP_BEGIN();
@@ -2179,7 +2342,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
             if (alpha < 1e-12) { qstat = AC_MINSTEP; ++qit; break; }
             // ---- update of the stage variables (rows were updated with the step)
             STAMP_BEGIN();
-            if (stage_lane) {
+            if (RES_SPLIT && !LEAN) {
+                // every part its variables and dynamics rows (same operations)
+                if (k <= N) {
+#pragma unroll
+                    for (int j = 0; j < BVS; ++j) {
+                        const int v = LR.var(j);
+                        if (v < NZ) S.dz[k][v] += alpha * S.ddz[k][v];
+                    }
+                    if (k < N) {
+#pragma unroll
+                        for (int jd = 0; jd < DRS; ++jd) {
+                            const int i = part + PARTS * jd;
+                            if (i < NX) S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
+                        }
+                    }
+                }
+            } else if (stage_lane) {
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) S.dz[k][i] += alpha * S.ddz[k][i];
                 if (k < N) {

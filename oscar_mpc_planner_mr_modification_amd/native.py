@@ -67,6 +67,8 @@ def _load():
     lib.mpcg_prepare_scenario.restype = C.c_int
     lib.mpcg_select_lowest_cost_device.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp]
     lib.mpcg_select_lowest_cost_device.restype = C.c_int
+    lib.mpcg_winner_records_device.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
+    lib.mpcg_winner_records_device.restype = C.c_int
     if lib.mpcg_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
@@ -253,6 +255,25 @@ def select_best_device(n_scenes, n_guesses, N, xtraj, pobj, exit_code, prev_traj
                                      _ptr(best), _ptr(objective), C.c_void_p(s.cuda_stream))
     _check(rc, "mpcg_select_best_device")
     return best, objective
+
+
+def winner_records_device(xtraj, utraj, pobj, best, n_guesses, out, stream=None):
+    """mpcg_winner_records_device: the selected planner's record per scene (one launch; the device
+    form of distributed.winner_records) into `out` [n_scenes][winner_width]."""
+    import torch
+
+    n_scenes = best.shape[0]
+    B, N1, nx = xtraj.shape
+    nu = utraj.shape[2]
+    assert B == n_scenes * n_guesses and out.shape[0] == n_scenes and out.shape[1] == N1 * nx + (N1 - 1) * nu + 2
+    for t in (xtraj, utraj, pobj, out):
+        assert t.dtype == torch.float64 and t.is_contiguous()
+    assert best.dtype == torch.int32 and best.is_contiguous()
+    s = stream if stream is not None else torch.cuda.current_stream(pobj.device)
+    rc = lib.mpcg_winner_records_device(n_scenes, n_guesses, N1 - 1, nx, nu, _ptr(xtraj), _ptr(utraj), _ptr(pobj),
+                                        _ptr(best), _ptr(out), C.c_void_p(s.cuda_stream))
+    _check(rc, "mpcg_winner_records_device")
+    return out
 
 
 def scenes_to_device(scenes, device):

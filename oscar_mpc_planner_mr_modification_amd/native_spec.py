@@ -130,7 +130,8 @@ ABI_VERSION = 6
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size", "mpcg_qp_mem_size",
            "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
-           "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device", "mpcg_release_stream_workspace",
+           "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device", "mpcg_winner_records_device",
+           "mpcg_release_stream_workspace",
            "mpcg_instance_traits")
 
 

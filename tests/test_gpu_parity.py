@@ -199,6 +199,27 @@ def test_select_best_matches_reference_rule(native, torch_dev, oracle_mod):
     np.testing.assert_allclose(obj.cpu().numpy(), hobj, rtol=1e-12, atol=1e-12)
 
 
+def test_winner_records_device_matches_host_rule(native, torch_dev):
+    """mpcg_winner_records_device == distributed.winner_records (the torch restatement), including
+    scenes without a successful planner (best -1: planner 0's record, index -1 kept) and the slack
+    model's six states."""
+    import torch
+    from oscar_mpc_planner_mr_modification_amd.distributed import winner_records, winner_width
+
+    rng = np.random.default_rng(11)
+    for S, G, N, nx, nu in ((7, 8, 20, 5, 2), (5, 3, 20, 6, 2), (4, 1, 30, 6, 3)):
+        xt = torch.from_numpy(rng.standard_normal((S * G, N + 1, nx))).to(torch_dev)
+        ut = torch.from_numpy(rng.standard_normal((S * G, N, nu))).to(torch_dev)
+        pobj = torch.from_numpy(rng.standard_normal(S * G)).to(torch_dev)
+        best = torch.from_numpy(rng.integers(-1, G, S).astype(np.int32)).to(torch_dev)
+        best[0] = -1
+        out = torch.full((S, winner_width(N, nx, nu)), np.nan, dtype=torch.float64, device=torch_dev)
+        native.winner_records_device(xt, ut, pobj, best, G, out)
+        torch.cuda.synchronize()
+        ref = winner_records(xt.cpu(), ut.cpu(), pobj.cpu(), best.cpu(), G)
+        assert torch.equal(out.cpu(), ref)
+
+
 def test_multipliers_carried_between_solves(native, torch_dev, oracle_mod):
     """Two consecutive control steps of the same planners: the second solve
     starts from the NLP multipliers the first one left in the capsule
