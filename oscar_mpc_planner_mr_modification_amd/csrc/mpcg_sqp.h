@@ -604,7 +604,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // state the residual pass has just computed, with the same operations, and one box-sum exchange,
     // loop and fold fewer per interior-point iteration (wasted only on the iteration that exits).
     // Measured (profiles/r03q_ab.jsonl, two alternating repetitions): C2 12.32 -> 11.97 ms, C1 10.61
-    // -> 10.43, C4 47.48 -> 45.38, C5 20.60 -> 19.46, JS 38.32 -> 37.17.  (MPCG_FUSE_BAR=0: A/B)
+    // -> 10.43, C4 47.48 -> 45.38, C5 20.60 -> 19.46, JS 38.32 -> 37.17; C3 20.30 -> 19.81
+    // (profiles/r03s_ab.jsonl).  (MPCG_FUSE_BAR=0: A/B)
 #ifndef MPCG_FUSE_BAR
 #define MPCG_FUSE_BAR 1
 #endif
@@ -623,6 +624,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     constexpr bool RES_SPLIT = MPCG_RES_SPLIT > 0 && FUSE_BAR && !C::COMPACT && PARTS > 1 && 2 * NB <= NZ &&
                                (PARTS == 3 || MPCG_RES_SPLIT > 1);
     constexpr int DRS = (NX + PARTS - 1) / PARTS;  // dynamics rows per part
+    // the feedback's new dynamics multipliers split over the parts too (MPCG_PIN_SPLIT=1, A/B only:
+    // measured slower, C2 11.69 -> 11.78 ms, C1 10.16 -> 10.22, C5 unchanged; profiles/r03s_ab.jsonl)
+#ifndef MPCG_PIN_SPLIT
+#define MPCG_PIN_SPLIT 0
+#endif
+    constexpr bool PIN_SPLIT = MPCG_PIN_SPLIT > 0 && RES_SPLIT && !LEAN && C::CHAIN_SPLIT;
     __shared__ LdsOf<C> S;
 #ifdef MPCG_LDS_PAD
     // occupancy experiment only: pad the LDS footprint
@@ -2026,6 +2033,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                         for (int i = 0; i < NX; ++i) {
                             if (k == 0) S.ddz[0][NU + i] = 0.0;
+                            if constexpr (PIN_SPLIT) continue;
                             double a = pmine[i];
 #pragma unroll
                             for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
@@ -2035,6 +2043,23 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         if (k == N - 1) {
 #pragma unroll
                             for (int u = 0; u < NU; ++u) S.ddz[N][u] = 0.0;
+                        }
+                    }
+                    if constexpr (PIN_SPLIT) {
+                        // the new dynamics multipliers, rows split over the parts like the chains' rows
+                        if (k < N) {
+                            double dxn[NX];
+#pragma unroll
+                            for (int i = 0; i < NX; ++i) dxn[i] = S.ddz[k + 1][NU + i];
+#pragma unroll
+                            for (int t = 0; t < RS; ++t) {
+                                if (!rv[t]) continue;
+                                const int i = rs[t];
+                                double a = pmine[i];
+#pragma unroll
+                                for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
+                                S.pin[k][i] = a;
+                            }
                         }
                     }
                 } else
