@@ -531,4 +531,81 @@ __device__ inline void mirror(double A[NZ][NZ], double eps, double dia_extra = 0
         }
 }
 
+// The sweeps of mirror() with the eigenvector rows split over the PARTS lanes of a stage: every
+// part applies the same rotations to its own copy of A (symmetrised upper triangle, from the
+// stage's part 0), and part p accumulates only the rows p, p + PARTS, ... of V (Vr[t] = row
+// p + PARTS t; rows past NA stay unused).  Per entry the operations of mirror(): bit-identical.
+template <int NZ, int NA, int PARTS>
+__device__ inline void mirror_rows(double A[NZ][NZ], double (&Vr)[(NA + PARTS - 1) / PARTS][NA], int part,
+                                   double dia_extra) {
+    constexpr int RV = (NA + PARTS - 1) / PARTS;
+#pragma unroll
+    for (int t = 0; t < RV; ++t)
+#pragma unroll
+        for (int j = 0; j < NA; ++j) Vr[t][j] = (part + PARTS * t == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0.0, dia = 0.0;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            dia += A[i][i] * A[i][i];
+            if (i == NA - 1) dia += dia_extra;
+#pragma unroll
+            for (int j = i + 1; j < NA; ++j) off += A[i][j] * A[i][j];
+        }
+        if (off <= 1e-32 * dia || off < 1e-300) break;
+#pragma unroll
+        for (int p = 0; p < NA - 1; ++p)
+#pragma unroll
+            for (int q = p + 1; q < NA; ++q) {
+                const double apq = A[p][q];
+                if (fabs(apq) >= 1e-300) {
+                    const double theta = 0.5 * (A[q][q] - A[p][p]) * frcp(apq);
+                    const double at = fabs(theta);
+                    double t = at < 1e150 ? frcp(at + fsqrt_pos(fma(at, at, 1.0))) : 0.5 * frcp(at);
+                    t = theta >= 0.0 ? t : -t;
+                    const double c = frsq(fma(t, t, 1.0)), sn = t * c;
+                    const double tau = sn * frcp(1.0 + c);
+                    A[p][p] -= t * apq;
+                    A[q][q] += t * apq;
+                    A[p][q] = 0.0;
+#pragma unroll
+                    for (int r = 0; r < NA; ++r) {
+                        if (r == p || r == q) continue;
+                        double& arp = r < p ? A[r][p] : A[p][r];
+                        double& arq = r < q ? A[r][q] : A[q][r];
+                        const double g = arp, h = arq;
+                        arp = g - sn * fma(g, tau, h);
+                        arq = h + sn * fma(-h, tau, g);
+                    }
+#pragma unroll
+                    for (int r = 0; r < RV; ++r) {
+                        const double g = Vr[r][p], h = Vr[r][q];
+                        Vr[r][p] = g - sn * fma(g, tau, h);
+                        Vr[r][q] = h + sn * fma(-h, tau, g);
+                    }
+                }
+            }
+    }
+}
+// mirror()'s reconstruction A = V diag(f(d)) V' from the eigenvalues on A's diagonal
+template <int NZ, int NA>
+__device__ inline void mirror_rebuild(double A[NZ][NZ], const double (&V)[NA][NA], double eps) {
+    double d[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        double di = A[i][i];
+        d[i] = (di >= -eps && di <= eps) ? eps : fabs(di);
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = i; j < NA; ++j) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) acc += V[i][k] * d[k] * V[j][k];
+            A[i][j] = acc;
+            A[j][i] = acc;
+        }
+}
+
 }  // namespace mpcg

@@ -211,33 +211,39 @@ __global__ __launch_bounds__(64) void prepare_kernel(mpcg_problem pr, int n_scen
     const double* base = in.stage_params + (size_t)sc * npar;
     double* P = params + (size_t)sol * N * npar;
     const int lin0 = pr.i_lin0, ell0 = pr.i_ell0;
-    // (stage, index) of element e = lane + 64 it, advanced without a division per element
-    int k = lane / npar, idx = lane - (lane / npar) * npar;
-    for (int e = lane; e < N * npar; e += 64) {
-        if (e > lane) {
-            idx += 64;
-            while (idx >= npar) { idx -= npar; ++k; }
-        }
-        double v = base[idx];
-        if (NL > 0 && idx >= lin0 && idx < lin0 + 3 * NL) {
-            const int i = (idx - lin0) / 3, c = (idx - lin0) - 3 * i;
-            if (guided && k >= 1 && i < n_obs) continue;  // written by the stage's DR lane
-            v = c == 0 ? 1.0 : (c == 1 ? 0.0 : __dadd_rn(x0, 100.0));
-        } else if (NE > 0 && idx >= ell0 && idx < ell0 + 7 * NE) {
-            const int j = (idx - ell0) / 7, c = (idx - ell0) - 7 * j;
-            if (k == 0) {
-                const double dummy[7] = {__dadd_rn(x0, 50.0), __dadd_rn(y0, 50.0), 0.0, 0.0, 0.0, 1.0, 0.1};
-                v = dummy[c];
-            } else {
-                const double* o = in.obst + (((size_t)sc * NE + j) * N + (k - 1)) * 5;
-                const double* m = in.obst_meta + ((size_t)sc * NE + j) * 2;
-                v = c < 5 ? o[c] : (c == 5 ? m[1] : m[0]);  // x y psi major minor | chi r
+    // lane <-> parameter index idx = c0 + lane of every stage: the scene's base row is read once per
+    // chunk and each stage's row is one coalesced store (no dependent global load per element)
+    for (int c0 = 0; c0 < npar; c0 += 64) {
+        const int idx = c0 + lane;
+        if (idx >= npar) break;
+        const double bv = base[idx];
+        const bool is_lin = NL > 0 && idx >= lin0 && idx < lin0 + 3 * NL;
+        const bool is_ell = !is_lin && NE > 0 && idx >= ell0 && idx < ell0 + 7 * NE;
+        const bool is_cons = !is_lin && !is_ell && pr.i_cons_w >= 0 &&
+                             (idx == pr.i_cons_w || idx == pr.i_prev_x || idx == pr.i_prev_y);
+        const int li = is_lin ? (idx - lin0) / 3 : 0, lc = is_lin ? (idx - lin0) - 3 * li : 0;
+        const int ej = is_ell ? (idx - ell0) / 7 : 0, ec = is_ell ? (idx - ell0) - 7 * ej : 0;
+#pragma unroll 4
+        for (int k = 0; k < N; ++k) {
+            double v = bv;
+            if (is_lin) {
+                if (guided && k >= 1 && li < n_obs) continue;  // written by the stage's DR lane
+                v = lc == 0 ? 1.0 : (lc == 1 ? 0.0 : __dadd_rn(x0, 100.0));
+            } else if (is_ell) {
+                if (k == 0) {
+                    const double dummy[7] = {__dadd_rn(x0, 50.0), __dadd_rn(y0, 50.0), 0.0, 0.0, 0.0, 1.0, 0.1};
+                    v = dummy[ec];
+                } else {
+                    const double* o = in.obst + (((size_t)sc * NE + ej) * N + (k - 1)) * 5;
+                    const double* m = in.obst_meta + ((size_t)sc * NE + ej) * 2;
+                    v = ec < 5 ? o[ec] : (ec == 5 ? m[1] : m[0]);  // x y psi major minor | chi r
+                }
+            } else if (is_cons) {
+                const bool on = cons && k >= 1 && k <= N - 2;
+                v = !on ? 0.0 : (idx == pr.i_cons_w ? in.w_consistency : L.prev[k][idx == pr.i_prev_x ? 0 : 1]);
             }
-        } else if (pr.i_cons_w >= 0 && (idx == pr.i_cons_w || idx == pr.i_prev_x || idx == pr.i_prev_y)) {
-            const bool on = cons && k >= 1 && k <= N - 2;
-            v = !on ? 0.0 : (idx == pr.i_cons_w ? in.w_consistency : L.prev[k][idx == pr.i_prev_x ? 0 : 1]);
+            P[(size_t)k * npar + idx] = v;
         }
-        P[e] = v;
     }
     double* W = warm + (size_t)sol * (N + 1) * MPCG_NVAR;
     for (int e = lane; e < (N + 1) * MPCG_NVAR; e += 64) W[e] = (&L.warm[0][0])[e];
@@ -479,6 +485,10 @@ __global__ __launch_bounds__(256) void scenario_prepare_kernel(mpcg_problem pr, 
             }
         };
         rebuild();
+        // lane r keeps round r's pick; the rows are formed after the rounds, one per lane (the
+        // same operations as forming each in lane 0 inside its round)
+        double pick_d = 0.0;
+        int pick_i = BIG;
         for (int r = 0; r < NS; ++r) {
             // wave arg-min of the list heads over (distance, index) through DPP
             double bd = td[0];
@@ -504,19 +514,23 @@ __global__ __launch_bounds__(256) void scenario_prepare_kernel(mpcg_problem pr, 
             if (__any(left > 0 && ti[0] == BIG)) {
                 if (left > 0 && ti[0] == BIG) rebuild();
             }
-            if (lane == 0) {
-                double a1 = 0.0, a2 = 0.0, b = 0.0;
-                if (found) {
-                    const double qx = q[2 * bi], qy = q[2 * bi + 1];
-                    const double dn = fmax(bd, 1e-9);
-                    a1 = __ddiv_rn(__dsub_rn(qx, rx), dn);
-                    a2 = __ddiv_rn(__dsub_rn(qy, ry), dn);
-                    b = __dsub_rn(__dadd_rn(__dmul_rn(a1, qx), __dmul_rn(a2, qy)), in.radius);
-                }
-                L.rows[k][r][0] = a1;
-                L.rows[k][r][1] = a2;
-                L.rows[k][r][2] = b;
+            if (lane == r) {
+                pick_d = bd;
+                pick_i = bi;
             }
+        }
+        if (lane < NS) {
+            double a1 = 0.0, a2 = 0.0, b = 0.0;
+            if (pick_i < M) {
+                const double qx = q[2 * pick_i], qy = q[2 * pick_i + 1];
+                const double dn = fmax(pick_d, 1e-9);
+                a1 = __ddiv_rn(__dsub_rn(qx, rx), dn);
+                a2 = __ddiv_rn(__dsub_rn(qy, ry), dn);
+                b = __dsub_rn(__dadd_rn(__dmul_rn(a1, qx), __dmul_rn(a2, qy)), in.radius);
+            }
+            L.rows[k][lane][0] = a1;
+            L.rows[k][lane][1] = a2;
+            L.rows[k][lane][2] = b;
         }
     }
     __syncthreads();

@@ -624,6 +624,15 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     constexpr bool RES_SPLIT = MPCG_RES_SPLIT > 0 && FUSE_BAR && !C::COMPACT && PARTS > 1 && 2 * NB <= NZ &&
                                (PARTS == 3 || MPCG_RES_SPLIT > 1);
     constexpr int DRS = (NX + PARTS - 1) / PARTS;  // dynamics rows per part
+    // MIRROR's eigenvector rows split over the parts of a stage (MPCG_MSPLIT=1, A/B only): bit-identical
+    // outputs (scripts/bitcmp.py on C2, C5, C4, JS: profiles/r03t_bitcmp.log) but slower everywhere --
+    // the stage matrix and row exchanges and the longer-lived state push the linearisation into
+    // scratch: C2 11.65 -> 12.46 ms, C1 10.16 -> 10.45, C4 45.41 -> 50.57, C5 19.47 -> 21.53, JS
+    // 37.24 -> 39.63, JD 40.56 -> 43.38 (profiles/r03t_ab.jsonl)
+#ifndef MPCG_MSPLIT
+#define MPCG_MSPLIT 0
+#endif
+    constexpr bool MSPLIT = MPCG_MSPLIT > 0 && C::MODEL == 0;
     // the feedback's new dynamics multipliers split over the parts too (MPCG_PIN_SPLIT=1, A/B only:
     // measured slower, C2 11.69 -> 11.78 ms, C1 10.16 -> 10.22, C5 unchanged; profiles/r03s_ab.jsonl)
 #ifndef MPCG_PIN_SPLIT
@@ -835,8 +844,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < 6; ++i) hb6[i] = acc[i];
             }
             double resl = 0.0;
+            // MSPLIT: the MIRROR sweeps run on all parts of a stage, each accumulating its rows of the
+            // eigenvectors (mirror_rows); the stage matrix goes out from part 0 and the other parts'
+            // rows come back through MX, a per-stage exchange area over the Riccati arrays P, Lc, Y
+            // and the box sums (all dead during the linearisation)
+            constexpr int MNA = NZ == 8 ? NZ - 1 : NZ;  // the slack model's decoupled slack diagonal aside
+            constexpr int MRV = (MNA + PARTS - 1) / PARTS;
+            constexpr int MXS = imax(MNA * (MNA + 1) / 2, (MNA - (MNA + PARTS - 1) / PARTS) * MNA) + 1;
+            double* const MX = &S.P[0][0];
+            static_assert(!MSPLIT || offsetof(LdsOf<C>, Dg) - offsetof(LdsOf<C>, P) >= sizeof(double) * N * MXS,
+                          "MIRROR exchange area (P, Lc, Y, bx)");
+            double H[NZ][NZ];
             if (stage_lane && k < N) {
-                double g[NZ], H[NZ][NZ], xn[NX], pi[NX];
+                double g[NZ], xn[NX], pi[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
                 if constexpr (C::MODEL == 1) {
@@ -883,7 +903,19 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 H[X1][X1] += hb6[3]; H[X1][X2] += hb6[4]; H[X2][X1] += hb6[4];
                 H[X2][X2] += hb6[5];
                 STAMP_LAP(13);
-                if constexpr (C::MODEL == 0 && NZ == 8) {
+                if constexpr (MSPLIT) {
+                    // mirror()'s symmetrisation, then the upper triangle (and the slack diagonal's
+                    // square, which enters the sweeps' convergence test) to the stage's exchange slot
+#pragma unroll
+                    for (int i = 0; i < MNA; ++i)
+#pragma unroll
+                        for (int j = i + 1; j < MNA; ++j) H[i][j] = 0.5 * (H[i][j] + H[j][i]);
+#pragma unroll
+                    for (int i = 0; i < MNA; ++i)
+#pragma unroll
+                        for (int j = i; j < MNA; ++j) MX[k * MXS + sym(j, i)] = H[i][j];
+                    MX[k * MXS + MXS - 1] = NZ == 8 ? H[NZ - 1][NZ - 1] * H[NZ - 1][NZ - 1] : 0.0;
+                } else if constexpr (C::MODEL == 0 && NZ == 8) {
                     // the slack row/column of the slack model is exactly zero off the
                     // diagonal (quadratic slack cost, linear in every h row, no dynamics
                     // coupling): MIRROR of the 8x8 block = MIRROR of the leading 7x7 block
@@ -920,7 +952,8 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     mirror<NZ>(H, pr.reg_eps);
                 }
                 STAMP_LAP(14);
-                if constexpr (C::COMPACT) {
+                if constexpr (MSPLIT) {
+                } else if constexpr (C::COMPACT) {
 #pragma unroll
                     for (int i = 0; i < NZ; ++i)
 #pragma unroll
@@ -942,6 +975,56 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = NU; i < NZ; ++i) {
                     if constexpr (C::COMPACT) Hb(N)[sym(i - 1, i - 1)] = pr.reg_eps;
                     else Hb(N)[sym(i, i)] = pr.reg_eps;
+                }
+            }
+            if constexpr (MSPLIT) {
+                wave_sync();
+                if (k < N) {
+                    double dx2 = 0.0;
+                    if (part != 0) {
+#pragma unroll
+                        for (int i = 0; i < MNA; ++i)
+#pragma unroll
+                            for (int j = i; j < MNA; ++j) H[i][j] = MX[k * MXS + sym(j, i)];
+                    }
+                    dx2 = MX[k * MXS + MXS - 1];
+                    double Vr[MRV][MNA];
+                    mirror_rows<NZ, MNA, PARTS>(H, Vr, part, dx2);
+                    wave_sync();  // every part has read the stage matrix
+                    if (part != 0) {
+#pragma unroll
+                        for (int t = 0; t < MRV; ++t) {
+                            const int r = part + PARTS * t;
+                            if (r >= MNA) continue;
+                            const int sl = r - 1 - (r - 1) / PARTS;  // rank among the rows of parts 1..
+#pragma unroll
+                            for (int j = 0; j < MNA; ++j) MX[k * MXS + sl * MNA + j] = Vr[t][j];
+                        }
+                    }
+                    wave_sync();
+                    if (part == 0) {
+                        double V[MNA][MNA];
+#pragma unroll
+                        for (int r = 0; r < MNA; ++r) {
+                            if (r % PARTS == 0) {
+#pragma unroll
+                                for (int j = 0; j < MNA; ++j) V[r][j] = Vr[r / PARTS][j];
+                            } else {
+                                const int sl = r - 1 - (r - 1) / PARTS;
+#pragma unroll
+                                for (int j = 0; j < MNA; ++j) V[r][j] = MX[k * MXS + sl * MNA + j];
+                            }
+                        }
+                        mirror_rebuild<NZ, MNA>(H, V, pr.reg_eps);
+                        if constexpr (NZ == 8) {
+                            const double hs = H[NZ - 1][NZ - 1];
+                            H[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
+                        }
+#pragma unroll
+                        for (int i = 0; i < NZ; ++i)
+#pragma unroll
+                            for (int j = 0; j <= i; ++j) Hb(k)[sym(i, j)] = H[i][j];
+                    }
                 }
             }
             res_eq = wave_max(resl);
