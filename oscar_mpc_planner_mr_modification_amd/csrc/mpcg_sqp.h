@@ -617,12 +617,14 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     // parts wait.  Same operations per row.  Measured (profiles/r03r_ab.jsonl, two alternating
     // repetitions): C2 11.99 -> 11.68 ms, C1 10.42 -> 10.15, C5 unchanged; on the two-part long
     // horizons it moves the allocation into scratch (C4 45.29 -> 46.76, JD 40.45 -> 40.70, JS
-    // 37.25 -> 37.13), so three-part instances only.  (MPCG_RES_SPLIT=0: off, 2: every instance)
+    // 37.25 -> 37.13), so three-part instances only; and not on the slack model, where it was neutral
+    // in time but moved the allocation into scratch (C5 52 -> 188 B/lane, 264 -> 782 MB of HBM traffic
+    // per launch, profiles/r03u_c5_pmc.json).  (MPCG_RES_SPLIT=0: off, 2: every instance)
 #ifndef MPCG_RES_SPLIT
 #define MPCG_RES_SPLIT 1
 #endif
     constexpr bool RES_SPLIT = MPCG_RES_SPLIT > 0 && FUSE_BAR && !C::COMPACT && PARTS > 1 && 2 * NB <= NZ &&
-                               (PARTS == 3 || MPCG_RES_SPLIT > 1);
+                               ((PARTS == 3 && NX == 5) || MPCG_RES_SPLIT > 1);
     constexpr int DRS = (NX + PARTS - 1) / PARTS;  // dynamics rows per part
     // MIRROR's eigenvector rows split over the parts of a stage (MPCG_MSPLIT=1, A/B only): bit-identical
     // outputs (scripts/bitcmp.py on C2, C5, C4, JS: profiles/r03t_bitcmp.log) but slower everywhere --
