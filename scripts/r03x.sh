@@ -8,3 +8,6 @@ for c in C5 JS JD C3 C4; do
   echo "bench $c done"
 done
 echo all-done
+timeout -k 10 300 python scripts/latency.py --config JS --guesses 5 > gpurun_out/r03x_latency_js.json 2> gpurun_out/r03x_latency_js.err || exit 1
+timeout -k 10 300 python scripts/latency.py --config C2 --guesses 8 > gpurun_out/r03x_latency_c2.json 2> gpurun_out/r03x_latency_c2.err || exit 1
+echo latency-done
