@@ -29,7 +29,12 @@ def main():
     from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
 
     lay = config_layout(a.config)
-    b = make_batch(lay, a.scenes, a.guesses, workers=16)
+    if a.config == "C3":
+        # the bicycle batch (one solve per scene)
+        from oscar_mpc_planner_mr_modification_amd.bicycle import make_c3_batch
+        b = make_c3_batch(lay, a.scenes)
+    else:
+        b = make_batch(lay, a.scenes, a.guesses, workers=16)
     dev = torch.device("cuda:0")
     B = b.params.shape[0]
     t = lambda x: torch.from_numpy(x).to(dev).contiguous()  # noqa: E731
