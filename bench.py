@@ -556,6 +556,14 @@ def main():
                                                    "frac": tf * lu / FP64_VALU_PEAK_TFLOPS}
     if "prepare" in phase_ms and hasattr(wl, "producer_roofline"):
         roofline["producer"] = wl.producer_roofline(phase_ms["prepare"])
+    # MFMA utilisation (north_star asks for it): zero by design -- no v_mfma in any kernel's ISA
+    # (scripts/isa_mfma_count.sh -> profiles/r04_isa_mfma.txt); DESIGN.md §3 "Why not MFMA"
+    roofline["mfma"] = {
+        "util": 0.0, "mfma_instructions_in_sqp_kernel": 0, "evidence": "profiles/r04_isa_mfma.txt",
+        "why": ("no condensing: the stage-banded QP is factorised by a Riccati recursion over "
+                f"{lay.nu + lay.nx}x{lay.nu + lay.nx} fp64 stage blocks, so there is no dense KKT GEMM; the blocks are far "
+                "below a 16x16x4 f64 MFMA tile, the recursion is a chain of dependent 2x2 pivots, and gfx950's "
+                "fp64 MFMA peak equals its fp64 vector peak, so MFMA could not raise this roofline")}
     ok = exit_h == 1
     stats = {"success_frac": float(ok.mean()), "rti_iters_per_solve": float(info_h[:, 0].mean()),
              "qp_iters_per_solve": float(info_h[:, 1].mean()), "qp_warm_start": args.qp_warm_start,

@@ -493,22 +493,41 @@ void orc_mirror(int n, double *H, double eps) {
         }
 }
 
-/* Arithmetic forms.  The default build computes the interior point with the GPU kernel's
- * arithmetic forms, most of which are HPIPM's / BLASFEO's own: the 2x2 Cholesky through
- * reciprocal square roots and multiplications by the inverted diagonal (BLASFEO's dpotrf
- * keeps inv_diag), barrier terms through t_inv = 1/t (HPIPM's Gamma = t_inv lam), the row
- * residual as D.dz + t - d, the step to the boundary as 1 / max(-dt/t, -dl/l), and the QP's
- * stationarity residual associated as the kernel's lane sums are.  These are rounding
- * choices of the same algorithm; they matter where an exit decision rests on rounding
- * (C5's dual-degenerate QPs, DESIGN.md §3.2: the convergence test there reads a residual
- * made of cancelling multipliers of 1e13 and more).  -DORC_LITERAL builds the literal
- * forms (divisions, row-order sums): the second build of the rounding-sensitivity record
- * (scripts/rounding_proxy.py, tests/test_rounding_record.py). */
-#ifdef ORC_LITERAL
-#define KF 0
+/* Arithmetic forms: three builds of the same interior-point algorithm that differ only in
+ * rounding (which operation forms and which summation order).  They matter only where an
+ * exit decision rests on rounding (C5's dual-degenerate QPs, DESIGN.md §3.2: the
+ * convergence test there reads a residual made of cancelling multipliers of 1e13 and more).
+ *
+ * ORC_FORMS 1 (default): HPIPM's / BLASFEO's own forms, none taken from the GPU kernel
+ *   (HPIPM and BLASFEO are acados submodules at a commit the reference does not pin; the
+ *   forms are restated from their published sources, version unpinned):
+ *   - Cholesky of the input block as BLASFEO's dpotrf_l: l_jj = sqrt(d), inv_diag_j =
+ *     1 / l_jj, sub-diagonal entries and the triangular solves multiplied by inv_diag;
+ *   - barrier terms through t_inv = 1 / t (HPIPM compute_Gamma_gamma: Gamma = t_inv lam);
+ *   - the row residual res_d = D.dz + t - d (HPIPM res_compute: the constraint product
+ *     first, then t and d added);
+ *   - the step to the boundary as HPIPM compute_alpha: alpha = min over rows of -t/dt and
+ *     -lam/dlam (one division per blocking row);
+ *   - the stationarity residual in HPIPM's evaluation order, res_g = (H dz + g) + (lam_u -
+ *     lam_l) on the box rows + D' lam of the general rows (row order) + [B A]' pi - pi_prev
+ *     (BLASFEO's gemv kernels block the sums by four; that association is not restated).
+ * ORC_FORMS 0 (-DORC_LITERAL): the literal forms -- divisions, row-order sums -- the second
+ *   kernel-agnostic build.
+ * ORC_FORMS 2 (-DORC_KERNEL_FORMS, diagnostic only): the GPU kernel's forms, including its
+ *   wavefront layout (the 2x2 pivot's 1/l11 = l00 / sqrt(det), 1 / max(-dt/t, -dl/l), the
+ *   h rows' stationarity sums folded per lane part).  Not used as the parity reference: a
+ *   build that copies the kernel's association is partly self-agreement.
+ * Records: scripts/parity_full.py (rounding-decided = the two kernel-agnostic builds part),
+ * tests/test_rounding_record.py. */
+#if defined(ORC_LITERAL)
+#define ORC_FORMS 0
+#elif defined(ORC_KERNEL_FORMS)
+#define ORC_FORMS 2
 #else
-#define KF 1
+#define ORC_FORMS 1
 #endif
+#define KF (ORC_FORMS >= 1) /* t_inv, res_d = D.dz + t - d, inv_diag Cholesky (HPIPM / BLASFEO) */
+#define KK (ORC_FORMS == 2) /* the kernel's own forms */
 
 /* ------------------------------------------------------------------ */
 /* OCP-QP: Riccati-based Mehrotra primal-dual interior point            */
@@ -577,40 +596,48 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
             m++;
         }
         if (KF) {
-            /* the kernel's association of the stationarity residual: (H dz + g) + (box
-             * multipliers: upper - lower per variable, plus the h rows' sums per lane part
-             * folded part 0 + part 1 + part 2), then + F' pi term by term, then - pi_prev */
-            const int parts = (64 / (N + 1)) >= 3 ? 3 : 2;
-            double rbox[NZ] = {0}, rh[3][NZ];
-            memset(rh, 0, sizeof rh);
-            for (int c = 0; c < S->ni; c++) {
-                if (S->hrow[c] < 0) {
-                    for (int i = 0; i < NZ; i++)
-                        if (S->D[c][i] != 0.0) rbox[i] += S->D[c][i] * S->lam[c]; /* lower (-l) then upper (+l) */
-                }
-            }
-            for (int i = 0; i < NZ; i++) rbox[i] = rbox[i] == 0.0 ? 0.0 : rbox[i];
-            /* upper - lower in the kernel's operand order */
+            /* box multipliers as upper - lower per variable (HPIPM res_compute: lam_u - lam_l,
+             * added at the box index) */
+            double rbox[NZ];
             for (int i = 0; i < NZ; i++) {
                 double lo = 0.0, hi = 0.0;
                 for (int c = 0; c < S->ni; c++)
                     if (S->hrow[c] < 0 && S->D[c][i] != 0.0) { if (S->D[c][i] > 0) hi = S->lam[c]; else lo = S->lam[c]; }
                 rbox[i] = hi - lo;
             }
-            for (int c = 0; c < S->ni; c++) {
-                if (S->hrow[c] < 0) continue;
-                const int pp = S->hrow[c] % parts;
-                for (int i = 0; i < NZ; i++) rh[pp][i] += S->D[c][i] * S->lam[c];
-            }
-            for (int i = 0; i < NZ; i++) {
-                double acc = rh[0][i];
-                for (int pp = 1; pp < parts; pp++) acc += rh[pp][i];
-                rbox[i] += acc;
-            }
-            for (int i = 0; i < NZ; i++) {
-                double a = 0.0;
-                for (int j = 0; j < NZ; j++) a += S->H[i][j] * S->dz[j];
-                r[i] = a + S->g[i] + rbox[i];
+            if (KK) {
+                /* diagnostic kernel-forms build: (H dz + g) + (box + the h rows' sums per lane
+                 * part folded part 0 + part 1 + part 2), then + F' pi term by term, - pi_prev */
+                const int parts = (64 / (N + 1)) >= 3 ? 3 : 2;
+                double rh[3][NZ];
+                memset(rh, 0, sizeof rh);
+                for (int c = 0; c < S->ni; c++) {
+                    if (S->hrow[c] < 0) continue;
+                    const int pp = S->hrow[c] % parts;
+                    for (int i = 0; i < NZ; i++) rh[pp][i] += S->D[c][i] * S->lam[c];
+                }
+                for (int i = 0; i < NZ; i++) {
+                    double acc = rh[0][i];
+                    for (int pp = 1; pp < parts; pp++) acc += rh[pp][i];
+                    rbox[i] += acc;
+                }
+                for (int i = 0; i < NZ; i++) {
+                    double a = 0.0;
+                    for (int j = 0; j < NZ; j++) a += S->H[i][j] * S->dz[j];
+                    r[i] = a + S->g[i] + rbox[i];
+                }
+            } else {
+                /* HPIPM's order: res_g = (H dz + g) (BLASFEO symv: the product, then beta y),
+                 * + box, + D' lam over the general rows in row order */
+                for (int i = 0; i < NZ; i++) {
+                    double a = 0.0;
+                    for (int j = 0; j < NZ; j++) a += S->H[i][j] * S->dz[j];
+                    r[i] = a + S->g[i] + rbox[i];
+                }
+                for (int c = 0; c < S->ni; c++) {
+                    if (S->hrow[c] < 0) continue;
+                    for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * S->lam[c];
+                }
             }
             if (k < N)
                 for (int m2 = 0; m2 < NX; m2++)
@@ -670,8 +697,8 @@ static int riccati_factor(qp_ws *w) {
                 for (int m = 0; m < NX; m++) acc += F[m][i] * PF[m][j];
                 M[i][j] = acc;
             }
-        if (KF && NU == 2) {
-            /* both reciprocal square roots from the block entries,
+        if (KK && NU == 2) {
+            /* kernel forms: both reciprocal square roots from the block entries,
              * 1/l11 = l00 / sqrt(m00 m11 - m10^2) */
             const double m00 = M[0][0], m10 = M[1][0], m11 = M[1][1];
             if (!(m00 > 0.0)) return -1;
@@ -691,17 +718,26 @@ static int riccati_factor(qp_ws *w) {
                     S->P[i][j] = M[NU + i][NU + j] - S->Y[0][i] * S->Y[0][j] - S->Y[1][i] * S->Y[1][j];
             continue;
         }
-        /* Cholesky of Muu (L L' = Muu) */
+        /* Cholesky of Muu (L L' = Muu).  HPIPM forms: BLASFEO dpotrf_l (sqrt, inv_diag = 1 /
+         * l_jj, entries multiplied by inv_diag); kernel forms: inv_diag = 1 / sqrt(d) first,
+         * l_jj = d inv_diag; literal: sqrt and divisions.  A pivot <= 0 fails the QP (NaN
+         * status): BLASFEO would continue with a zero inverse, DESIGN.md §2.2. */
         for (int j = 0; j < NU; j++) {
             double d = M[j][j];
             for (int m = 0; m < j; m++) d -= S->L[j][m] * S->L[j][m];
             if (!(d > 0.0)) return -1;
-            d = sqrt(d);
+            if (KK) {
+                S->il[j] = 1.0 / sqrt(d);
+                d = d * S->il[j];
+            } else {
+                d = sqrt(d);
+                S->il[j] = 1.0 / d;
+            }
             S->L[j][j] = d;
             for (int i = j + 1; i < NU; i++) {
                 double acc = M[i][j];
                 for (int m = 0; m < j; m++) acc -= S->L[i][m] * S->L[j][m];
-                S->L[i][j] = acc / d;
+                S->L[i][j] = KF ? acc * S->il[j] : acc / d;
             }
             for (int i = 0; i < j; i++) S->L[i][j] = 0.0;
         }
@@ -710,7 +746,7 @@ static int riccati_factor(qp_ws *w) {
             for (int i = 0; i < NU; i++) {
                 double acc = M[i][NU + j];
                 for (int m = 0; m < i; m++) acc -= S->L[i][m] * S->Y[m][j];
-                S->Y[i][j] = acc / S->L[i][i];
+                S->Y[i][j] = KF ? acc * S->il[i] : acc / S->L[i][i];
             }
         for (int i = 0; i < NX; i++)
             for (int j = 0; j < NX; j++) {
@@ -747,7 +783,7 @@ static void riccati_solve(qp_ws *w) {
         for (int i = 0; i < NU; i++) { /* y = L^{-1} m_u */
             double acc = m[i];
             for (int q = 0; q < i; q++) acc -= S->L[i][q] * S->y[q];
-            S->y[i] = (KF && NU == 2) ? acc * S->il[i] : acc / S->L[i][i];
+            S->y[i] = KF ? acc * S->il[i] : acc / S->L[i][i];
         }
         for (int i = 0; i < NX; i++) {
             double acc = m[NU + i];
@@ -768,7 +804,7 @@ static void riccati_solve(qp_ws *w) {
         for (int i = NU - 1; i >= 0; i--) { /* L' du = -c */
             double acc = -c[i];
             for (int q = i + 1; q < NU; q++) acc -= S->L[q][i] * du[q];
-            du[i] = (KF && NU == 2) ? acc * S->il[i] : acc / S->L[i][i];
+            du[i] = KF ? acc * S->il[i] : acc / S->L[i][i];
         }
         for (int i = 0; i < NU; i++) S->ddz[i] = du[i];
         for (int i = 0; i < NX; i++) S->ddz[NU + i] = (k == 0) ? 0.0 : dx[i];
@@ -822,8 +858,8 @@ static void ineq_steps(qp_ws *w, double *dtv_unused) {
 }
 
 static double max_step(qp_ws *w) {
-    if (KF) {
-        /* kernel: 1 / max over rows of -dt/t and -dl/l */
+    if (KK) {
+        /* kernel forms: 1 / max over rows of -dt/t and -dl/l */
         double rmax = 0.0;
         for (int k = 0; k <= w->N; k++) {
             qp_stage *S = &w->st[k];
@@ -972,9 +1008,11 @@ static int h_side(const double *uh, int r) { return uh[r] < BIGBOUND ? 1 : 0; }
 
 /* NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
  * multipliers the NLP holds: dynamics pi, row multipliers lr[k][c] */
-static void nlp_residuals(qp_ws *w, double *const *lr, double *rstat, double *rineq, double *rcomp) {
+static void nlp_residuals(qp_ws *w, double *const *lr, double *rstat, double *rineq, double *rcomp,
+                          int *nonfinite) {
     int N = w->N;
     double s_max = 0.0, i_max = 0.0, c_max = 0.0;
+    int bad = 0; /* a non-finite operand (the max tests below drop NaN) */
     for (int k = 0; k <= N; k++) {
         qp_stage *S = &w->st[k];
         double r[NZ];
@@ -991,12 +1029,17 @@ static void nlp_residuals(qp_ws *w, double *const *lr, double *rstat, double *ri
             for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * lr[k][c];
             if (-S->d[c] > i_max) i_max = -S->d[c];
             if (fabs(lr[k][c] * S->d[c]) > c_max) c_max = fabs(lr[k][c] * S->d[c]);
+            bad |= !isfinite(S->d[c]) || !isfinite(lr[k][c]);
         }
         int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
         for (int i = i0; i < i1; i++)
             if (fabs(r[i]) > s_max) s_max = fabs(r[i]);
+        for (int i = 0; i < NZ; i++) bad |= !isfinite(r[i]);
+        if (k < N)
+            for (int i = 0; i < NX; i++) bad |= !isfinite(S->b[i]);
     }
     *rstat = s_max; *rineq = i_max; *rcomp = c_max;
+    *nonfinite = bad;
 }
 
 /* SQP preparation phase: the QP of the iterate z (cost gradient / exact Hessian with
@@ -1173,8 +1216,14 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
                 lrp[k][c] = have_qp ? S->lam[c]
                                     : (S->hrow[c] >= 0 ? lamh[(size_t)k * 2 * nh + 2 * S->hrow[c] + S->hsgn[c]] : 0.0);
         }
-        nlp_residuals(&w, lrp, &res_stat, &res_ineq, &res_comp);
+        int nonfinite = 0;
+        nlp_residuals(&w, lrp, &res_stat, &res_ineq, &res_comp, &nonfinite);
         if (sqp_mode) {
+            /* a non-finite NLP residual ends the call with the NaN status (the kernel's guard) */
+            if (nonfinite) {
+                acados_status = AC_NAN;
+                break;
+            }
             /* acados SQP termination at this linearisation point */
             if (res_stat < pr->nlp_tol && res_eq < pr->nlp_tol && res_ineq < pr->nlp_tol && res_comp < pr->nlp_tol) {
                 acados_status = AC_SUCCESS;

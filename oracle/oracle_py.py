@@ -19,12 +19,16 @@ LIB_SLACK = os.path.join(HERE, "libmpcg_oracle_slack.so")
 LIB_BICYCLE = os.path.join(HERE, "libmpcg_oracle_bicycle.so")
 LIBS = {"unicycle": LIB, "unicycle_slack": LIB_SLACK, "bicycle_ca": LIB_BICYCLE}
 MODEL_DIMS = {"unicycle": (5, 2), "unicycle_slack": (6, 2), "bicycle_ca": (6, 3)}
-# the literal-forms builds (-DORC_LITERAL: divisions and row-order sums; mpcg_oracle.c
-# "Arithmetic forms"): the second build of the rounding-sensitivity record
-for _m, _f in (("unicycle", "libmpcg_oracle_literal.so"), ("unicycle_slack", "libmpcg_oracle_slack_literal.so"),
-               ("bicycle_ca", "libmpcg_oracle_bicycle_literal.so")):
-    LIBS[_m + "_literal"] = os.path.join(HERE, _f)
-    MODEL_DIMS[_m + "_literal"] = MODEL_DIMS[_m]
+# arithmetic-form builds (mpcg_oracle.c "Arithmetic forms"): the default builds use HPIPM's /
+# BLASFEO's forms; "_literal" (-DORC_LITERAL: divisions and row-order sums) is the second
+# kernel-agnostic build of the rounding-sensitivity record; "_kernel" (-DORC_KERNEL_FORMS: the
+# GPU kernel's forms and lane association) is diagnostic only
+FORMS = ("hpipm", "literal", "kernel")
+for _m, _stem in (("unicycle", "libmpcg_oracle"), ("unicycle_slack", "libmpcg_oracle_slack"),
+                  ("bicycle_ca", "libmpcg_oracle_bicycle")):
+    for _forms in FORMS[1:]:
+        LIBS[_m + "_" + _forms] = os.path.join(HERE, f"{_stem}_{_forms}.so")
+        MODEL_DIMS[_m + "_" + _forms] = MODEL_DIMS[_m]
 
 ORC_MAX_NU, ORC_MAX_NX = 3, 6
 
@@ -151,14 +155,20 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
 class Oracle:
     """Thin wrapper: stage functions and full solves on numpy arrays."""
 
-    def __init__(self, layout, literal=False, **opts):
-        """literal=True: the literal-forms build (rounding-sensitivity records only)"""
+    def __init__(self, layout, literal=False, forms="hpipm", **opts):
+        """forms: "hpipm" (default: HPIPM's / BLASFEO's arithmetic forms), "literal" (the second
+        kernel-agnostic build; literal=True is the same) or "kernel" (diagnostic: the GPU kernel's
+        forms) -- rounding-sensitivity records only"""
+        if literal:
+            forms = "literal"
+        assert forms in FORMS, forms
+        self.forms = forms
         self.layout = layout
         self.pr = problem_from_layout(layout, **opts)
         self.nx = nx = layout.nx
         self.nu = layout.nu
         self.nz = nx + self.nu
-        self.L = lib(layout.model + ("_literal" if literal else ""))
+        self.L = lib(layout.model + ("" if forms == "hpipm" else "_" + forms))
 
     @property
     def nh(self):

@@ -38,20 +38,33 @@ class ControlLoop:
         LS = 5 + layout.nh
         self.lam = torch.zeros((self.S * self.G, layout.N, LS), dtype=torch.float64, device=device)
         self.last = None
+        self.existing = None
 
-    def set_scene_data(self, state, obst, guidance):
-        """Replace the externally provided scene data (device tensors or arrays)."""
+    def set_scene_data(self, state, obst, guidance, existing_guidance=None):
+        """Replace the externally provided scene data (device tensors or arrays).
+
+        existing_guidance (S, G) bool, optional: which guided planners' guidance existed in the
+        previous step -- in the reference a planner keeps its guidance only when the homotopy
+        class guidance_planner finds this step maps back to the same planner
+        (guidance_constraints.cpp:211-257), so it comes from the guidance search, outside the
+        planner.  Read by the next step() with warmstart_with_mpc_solution (such a planner
+        starts from its own previous output, the others from their guidance); when not given,
+        every guided planner's guidance is taken to have existed (each kept its class)."""
         import torch
 
         t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=self.dev).contiguous()  # noqa: E731
         self.dsc["state"], self.dsc["obst"], self.dsc["guidance"] = t(state), t(obst), t(guidance)
+        self.existing = None
+        if existing_guidance is not None:
+            ex = torch.as_tensor(existing_guidance, device=self.dev).reshape(self.S, self.G)
+            self.existing = ex.to(torch.uint8).contiguous()
 
     def step(self, stream=None):
         """One control step of every scene.  Returns dict(best, exit, xtraj, utraj, pobj, objective, prepared)."""
         pr, S, G, N = self.pr, self.S, self.G, self.lay.N
         if self.own_warm and self.last is not None:
             self.dsc["planner_xtraj"], self.dsc["planner_utraj"] = self.last["xtraj"], self.last["utraj"]
-            self.dsc["existing_guidance"] = self.dsc["guided"]
+            self.dsc["existing_guidance"] = self.dsc["guided"] if self.existing is None else self.existing
         prep = native.prepare_device(pr, self.dsc, self.rr, self.wc, self.dec, stream=stream,
                                      warmstart_with_mpc_solution=self.own_warm, shift_forward=self.shift)
         out = native.solve_batch_device(pr, prep["params"], prep["warm"], prep["xinit"], stream=stream,

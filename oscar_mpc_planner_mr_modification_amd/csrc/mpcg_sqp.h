@@ -127,18 +127,25 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
-    // 1/t of every row kept in registers when the row state is small (up to 14 slots: C1, C2,
-    // C5, JS, JD); the instances with more row slots per lane (C4 20, C3 16) recompute it, which
-    // keeps them out of scratch.  Measured (scripts/ab_bench.py, profiles/r03d_ab_*): JS 42.11 ->
-    // 41.39 ms, C5 20.89 -> 20.68, JD unchanged; the stored variant of the two-part instances
-    // passed full-size parity (JS, JD: 20,480 solves each, profiles/r03c_variant_storeit.jsonl).
-    // Without it JD and C5 are scratch-free (68 / 28 B/lane with it) but slower: JD 44.47 -> 44.84
-    // ms, C5 20.69 -> 20.91 (profiles/r03k_ab.jsonl, MPCG_STORE_IT_MAX=12).
-    // MPCG_STORE_IT_MAX=0 recomputes it everywhere.
+    // 1/t of every row kept in registers when the row state is small (up to 14 slots) on the
+    // three-part instances (C1, C2, C5); the instances with more row slots per lane (C4 20, C3 16)
+    // recompute it, which keeps them out of scratch.  The two-part instances (JS, JD) recompute it
+    // too: the round-2 build that stored 1/t on a two-part instance computed wrong trajectories
+    // and faulted once, and its cause was never named, so the gate stays until it
+    // is.  Measured with the gate lifted (-DMPCG_STORE_IT_ANY; scripts/ab_bench.py,
+    // profiles/r03d_ab_*): JS 42.11 -> 41.39 ms, JD unchanged; full-size parity passed that way
+    // (profiles/r03c_variant_storeit.jsonl).  C5 stored: 20.89 -> 20.68 ms.  Without it C5 is
+    // scratch-free (28 B/lane with it) but slower, 20.69 -> 20.91 (profiles/r03k_ab.jsonl,
+    // MPCG_STORE_IT_MAX=12).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 14
 #endif
-    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
+#ifdef MPCG_STORE_IT_ANY
+    static constexpr bool STORE_IT_PARTS_OK = true;
+#else
+    static constexpr bool STORE_IT_PARTS_OK = PARTS == 3;
+#endif
+    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX && STORE_IT_PARTS_OK;
     // box bounds selected per use instead of held in registers (LaneBounds; MPCG_BOUNDS_SEL=1, A/B
     // only): C2 went into scratch with it (0 -> 68 B/lane), C3 unchanged, and C4 (148 -> 132 B/lane
     // of scratch) measured 50.75 vs 50.72 ms in two alternating repetitions (profiles/r03k_ab.jsonl)
@@ -819,6 +826,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0, n_maxit = 0;
     double res_eq = 0.0;
     double nlp_stat = 0.0, nlp_ineq = 0.0, nlp_comp = 0.0;  // NLP residuals of the last linearisation
+    bool nlp_nonfinite = false;
 
     for (int it = 0; sqp_mode || it < pr.sqp_iters; ++it) {
         // parameter loads are re-issued where they are used rather than hoisted out of
@@ -1047,6 +1055,9 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
             for (int i = 0; i < NB; ++i) rh[i] = 0.0;
             double vin = 0.0, vcp = 0.0, vst = 0.0;
+            // non-finite guard: 0 x every residual operand is NaN iff the operand is not finite (the
+            // fmax reductions below drop NaN, so a NaN iterate could otherwise pass the SQP test)
+            double chk = 0.0;
 #pragma unroll
             for (int j = 0; j < BVS; ++j) {
                 double lb = 0.0;
@@ -1054,6 +1065,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     const double zv = S.z[k][LR.var(j)];
                     const double gl = zv - LR.lo_at(j), gh = LR.hi_at(j) - zv;
                     const double ll = have_qp ? R.l[2 * j] : 0.0, lh = have_qp ? R.l[2 * j + 1] : 0.0;
+                    chk += 0.0 * (zv + ll + lh);
                     vin = fmax(vin, -gl);
                     vin = fmax(vin, -gh);
                     vcp = fmax(vcp, fabs(ll * gl));
@@ -1074,6 +1086,7 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 if constexpr (NB == 4) rh[3] += C::slack_coef(hh) * lam;
                 vin = fmax(vin, -gap);
                 vcp = fmax(vcp, fabs(lam * gap));
+                chk += 0.0 * (gap + lam);
             }
             double acc[NB];
 #pragma unroll
@@ -1105,14 +1118,26 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 for (int i = 0; i < NZ; ++i) {
                     const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
                     if (free_var) vst = fmax(vst, fabs(r[i]));
+                    chk += 0.0 * r[i];
+                }
+                if (k < N) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) chk += 0.0 * S.b[k][i];  // res_eq's operands
                 }
             }
             nlp_stat = wave_max(vst);
             nlp_ineq = wave_max(vin);
             nlp_comp = wave_max(vcp);
+            nlp_nonfinite = !(wave_sum(chk) == 0.0);
             wave_sync();
         }
         if (sqp_mode) {
+            // a non-finite NLP residual ends the call with the NaN status (an iterate gone non-finite
+            // after an applied max-iter QP step would otherwise run every remaining iteration)
+            if (nlp_nonfinite) {
+                acados_status = AC_NAN;
+                break;
+            }
             // acados SQP: converged at this linearisation point, or out of iterations (its
             // residuals and res_eq are the final iterate's either way)
             if (nlp_stat < pr.nlp_tol && res_eq < pr.nlp_tol && nlp_ineq < pr.nlp_tol && nlp_comp < pr.nlp_tol) {

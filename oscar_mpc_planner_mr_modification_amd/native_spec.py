@@ -90,6 +90,13 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     return pr
 
 
+def needs_full(pr: MpcgProblem) -> bool:
+    """whether a launch of `pr` runs the FULL kernel variant whatever buffers it is given
+    (mpcg_sqp.h needs_full: a full SQP call, or a first QP that starts warm); otherwise the
+    lean variant runs unless the call passes QP memory or a stats buffer"""
+    return pr.nlp_solver == NLP_SOLVER["SQP"] or (pr.qp_warm_start == 2 and bool(pr.qp_warm_first))
+
+
 class MpcgIo(C.Structure):
     """Mirror of `mpcg_io` (include/mpcg.h)."""
     _fields_ = [("params", C.c_void_p), ("warm", C.c_void_p), ("xinit", C.c_void_p), ("lam_in", C.c_void_p),

@@ -43,22 +43,39 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     warm_start_first_qp (default: warm-start the first QP too when ws == 2, the restated
     warm start; ws 2 with warm_first 0 is the reference's configuration, cold in SQP-RTI);
     literal: compare against the literal-forms oracle build instead; solver_type "SQP": one
-    full acados SQP call per solve"""
+    full acados SQP call per solve.
+
+    Two GPU launches of the same batch: the product path (`solve_batch_device` without the
+    stats buffer -- the lean kernel variant that bench.py and mpcg_solve_batch_device run;
+    the FULL variant where the configuration needs it: full SQP, a warm first QP) is the one
+    every exit / trajectory figure compares; the FULL variant (stats buffer: the NLP residuals,
+    what the drop-in's AcadosInfo reads) gives the residual figures and is compared with the
+    product launch bit for bit ("lean_full_*")."""
     if warm_first is None:
         warm_first = int(ws == 2)
     import torch
 
     import oracle_py
     from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.native_spec import needs_full
 
     lay, b = inputs(cfg, S, first)
     dev = torch.device("cuda:0")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     opts = dict(qp_warm_start=ws, qp_warm_first=warm_first, solver_type=solver_type)
     pr = native.problem_from_layout(lay, **opts)
-    out = native.solve_batch_device(pr, t(b.params), t(b.warm), t(b.xinit), stats=True)
+    P, W, X = t(b.params), t(b.warm), t(b.xinit)
+    out = native.solve_batch_device(pr, P, W, X)
+    full = native.solve_batch_device(pr, P, W, X, stats=True)
     torch.cuda.synchronize()
     got = {k: v.cpu().numpy() for k, v in out.items()}
+    gfull = {k: v.cpu().numpy() for k, v in full.items()}
+    got["stats"] = gfull["stats"]
+    variant = "full" if needs_full(pr) else "lean"
+    lean_full = {"lean_full_exit_equal": bool(np.array_equal(got["exit"], gfull["exit"])),
+                 "lean_full_info_equal": bool(np.array_equal(got["info"], gfull["info"])),
+                 "lean_full_xtraj_bit_equal": bool(np.array_equal(got["xtraj"], gfull["xtraj"])),
+                 "lean_full_max_abs_dx": float(np.abs(got["xtraj"] - gfull["xtraj"]).max())}
     t0 = time.time()
     ref = oracle_py.Oracle(lay, literal=literal, **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
     t_orc = time.time() - t0
@@ -88,9 +105,17 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     det = ~decided
     dx_lit = np.abs(got["xtraj"] - lit["xtraj"]).reshape(len(same), -1).max(1)
     ends_like_a_build = ((got["exit"] == ref["status"]) | (got["exit"] == lit["status"]))
+    # diagnostic third build: the GPU kernel's own forms (never the reference; it tells whether a
+    # GPU / oracle difference is the kernel's rounding)
+    kf = oracle_py.Oracle(lay, forms="kernel", **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
+    dxk = np.abs(got["xtraj"] - kf["xtraj"]).reshape(len(same), -1).max(1)
+    same_k = got["exit"] == kf["status"]
     capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
     return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "solver_type": solver_type,
-            "oracle": "literal" if literal else "default",
+            "oracle": "literal" if literal else "default (HPIPM forms)", "gpu_variant": variant, **lean_full,
+            "kernel_forms_exit_agreement": float(same_k.mean()),
+            "kernel_forms_max_abs_dx_success": float(dxk[same_k & (got["exit"] == 1)].max())
+            if (same_k & (got["exit"] == 1)).any() else None,
             "sqp_iter_agreement": float((got["info"][:, 0] == ref["sqp_iter"]).mean()),
             "solves": int(len(same)), "exit_agreement": float(same.mean()),
             "max_abs_dx_success_same_path": float(dx[path_ok].max()) if path_ok.any() else None,

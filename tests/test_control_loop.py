@@ -25,17 +25,31 @@ def _next_state(xtraj, best, state, G):
     return nxt
 
 
-def cpu_loop(lay, sc, steps, oracle_mod, prod_oracle, own_warm=False):
+def existing_at(sc, step, new_guidance):
+    """existing_guidance of a step: every guided planner kept its homotopy class, except, with
+    new_guidance, planner (0, 1) at step 1 and planner (1, 0) at step 2, whose guidance is new
+    that step (guidance_constraints.cpp:211-257: no planner had that class before)"""
+    ex = sc.guided.copy()
+    if new_guidance:
+        if step == 1:
+            ex[0, 1] = False
+        if step == 2:
+            ex[1, 0] = False
+    return ex
+
+
+def cpu_loop(lay, sc, steps, oracle_mod, prod_oracle, own_warm=False, new_guidance=False):
     S, G, N = sc.n_scenes, sc.n_guesses, lay.N
     orc = oracle_mod.Oracle(lay)
     lam = np.zeros((S * G, N, 5 + lay.nh))
     hist = []
     prev = None
-    for _ in range(steps):
+    for t in range(steps):
         if own_warm and prev is not None:
-            # t-mpc.warmstart_with_mpc_solution: every guided planner's guidance existed last step
+            # t-mpc.warmstart_with_mpc_solution: the guided planners whose guidance existed last step
+            # start from their own previous output
             sc.planner_xtraj, sc.planner_utraj = prev["xtraj"], prev["utraj"]
-            sc.existing_guidance = sc.guided.copy()
+            sc.existing_guidance = existing_at(sc, t, new_guidance)
         p = prod_oracle.prepare(lay, sc, ROBOT_RADIUS, W_CONS, DECELERATION, warmstart_with_mpc_solution=own_warm)
         r = orc.solve_batch(p["params"], p["warm"], p["xinit"], lam_in=lam, return_lam=True)
         best, obj = find_best_planner_host(S, G, N, r["xtraj"], r["pobj"], r["status"], p["prev_interp"], W_CONS,
@@ -79,10 +93,13 @@ def test_cpu_loop_bookkeeping(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,S,G,n_obs,own_warm", [("C2", 6, 8, None, False), ("C1", 4, 5, 3, False),
-                                                    ("C2", 6, 8, None, True)])
-def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs, own_warm):
-    """own_warm: t-mpc.warmstart_with_mpc_solution on (guidance_constraints.cpp:335-338)"""
+@pytest.mark.parametrize("cfg,S,G,n_obs,own_warm,new_guidance", [
+    ("C2", 6, 8, None, False, False), ("C1", 4, 5, 3, False, False), ("C2", 6, 8, None, True, False),
+    ("C2", 6, 8, None, True, True)])
+def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs, own_warm, new_guidance):
+    """own_warm: t-mpc.warmstart_with_mpc_solution on (guidance_constraints.cpp:335-338);
+    new_guidance: a guided planner whose guidance is new in a later step (existing_guidance 0,
+    supplied by the caller through set_scene_data) starts from its guidance, not its own plan"""
     import copy
 
     import producers_oracle
@@ -92,7 +109,8 @@ def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs, own_war
     lay = config_layout(cfg)
     steps = 3
     sc0 = make_scenes(lay, S, G, n_obs=n_obs, seed=2024)
-    ref = cpu_loop(lay, copy.deepcopy(sc0), steps, oracle_mod, producers_oracle, own_warm=own_warm)
+    ref = cpu_loop(lay, copy.deepcopy(sc0), steps, oracle_mod, producers_oracle, own_warm=own_warm,
+                   new_guidance=new_guidance)
     dev = torch.device("cuda:0")
     loop = ControlLoop(lay, sc0, dev, ROBOT_RADIUS, W_CONS, SEL_W, DECELERATION, warmstart_with_mpc_solution=own_warm)
     sc = sc0
@@ -114,5 +132,6 @@ def test_gpu_control_loop_matches_cpu_loop(oracle_mod, cfg, S, G, n_obs, own_war
             main_warm=c["main_warm"].cpu().numpy(), prev_traj=c["prev_traj"].cpu().numpy(),
             prev_elapsed=c["prev_elapsed"].cpu().numpy(), consistency_on=c["consistency_on"].cpu().numpy() > 0,
             previously_selected=c["previously_selected"].cpu().numpy() > 0, lam=None))
-        loop.set_scene_data(nxt.state, nxt.obst, nxt.guidance)
+        loop.set_scene_data(nxt.state, nxt.obst, nxt.guidance,
+                            existing_guidance=existing_at(nxt, t + 1, new_guidance) if new_guidance else None)
         sc = nxt
