@@ -59,7 +59,8 @@ sys.path.insert(0, ROOT)
 METRIC = "SQP solves/s (N=20, 8 obs, 8 guesses) at 1/2/4/8 MI355X; max |x−x_ref|"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (vendor spec)
-DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048, "JS": 4096, "JD": 4096}
+DEFAULT_SCENES = {"C1": 1024, "C2": 1024, "C3": 4096, "C4": 2048, "C5": 2048, "JS": 4096, "JD": 4096,
+                  "T10": 2048}  # T10: diagnostic shape for register-budget A/B runs, not a BASELINE config
 # jackalsimulator / jackal / dingo as shipped: n_paths 4 + the non-guided planner
 DEFAULT_GUESSES = {"JS": 5, "JD": 5}
 CHECK_CHUNK = 256              # solves per oracle call in the check leg

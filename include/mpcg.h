@@ -37,7 +37,7 @@ extern "C" {
 #define MPCG_NU 2            /* the unicycle models */
 #define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 6
+#define MPCG_ABI_VERSION 7
 /* mpcg_problem.model */
 #define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
 #define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
@@ -97,6 +97,11 @@ typedef struct mpcg_problem {
                                       stationarity, dynamics, inequality and complementarity residuals */
     int qp_warm_first;             /* acados warm_start_first_qp (default 0): the first QP of a call also starts
                                       warm (from mpcg_io.qp_in, or in SQP-RTI from the previous iteration's QP) */
+    /* ABI 7 */
+    double qp_t_min;               /* floor of every inequality row's slack t and multiplier lambda after each
+                                      interior-point step (HPIPM's t_min / lam_min safeguard; 1e-12 here, where
+                                      the dual-degenerate SH-MPC QPs' exit decisions stop depending on rounding,
+                                      DESIGN.md §2.2); 0 = no floor */
 } mpcg_problem;
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,

@@ -986,8 +986,10 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
             if (k < N)
                 for (int i = 0; i < NX; i++) S->pi[i] += alpha * (S->pin[i] - S->pi[i]);
             for (int c = 0; c < S->ni; c++) {
-                S->t[c] += alpha * S->dt[c];
-                S->lam[c] += alpha * S->dl[c];
+                /* the step, then the t / lambda floor qp_t_min */
+                const double tn = S->t[c] + alpha * S->dt[c], ln = S->lam[c] + alpha * S->dl[c];
+                S->t[c] = tn < pr->qp_t_min ? pr->qp_t_min : tn;
+                S->lam[c] = ln < pr->qp_t_min ? pr->qp_t_min : ln;
             }
         }
     }

@@ -388,6 +388,8 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->nlp_solver = MPCG_NLP_SQP_RTI;
     pr->nlp_max_iter = 100;
     pr->nlp_tol = 1e-2;
+    // the interior point's t / lambda floor
+    pr->qp_t_min = 1e-12;
     return 0;
 }
 

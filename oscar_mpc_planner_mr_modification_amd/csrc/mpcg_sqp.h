@@ -597,8 +597,14 @@ __host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
 // state is rewritten at every QP start and dead across the linearisation, which keeps
 // the register allocation of the hot loops (the warm start and the residual pass hold
 // the previous QP's row state across the linearisation).
+// MPCG_WAVES_PER_EU (register-budget experiments only): the allocator's target waves per SIMD
+#ifdef MPCG_WAVES_PER_EU
+#define MPCG_KERNEL_ATTR __launch_bounds__(MPCG_WG_LANES) __attribute__((amdgpu_waves_per_eu(MPCG_WAVES_PER_EU, MPCG_WAVES_PER_EU)))
+#else
+#define MPCG_KERNEL_ATTR __launch_bounds__(64, 1)
+#endif
 template <class C, bool FULL = false>
-__global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
+__global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps,
                                                     double* __restrict__ gws) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
@@ -1551,10 +1557,25 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                 if (phase == 0) {
                     constexpr int NT = C::NTRI, NP = C::NPT, DZ = C::NDH - 1;
                     constexpr bool FAC_FLAT = C::FAC_FLAT;
+                    // FAC_PAIR: two lanes per block entry (lanes 2e, 2e + 1 of entry e), each forming the
+                    // cost-to-go product P F[:, ej] on half of the rows (0-2 / 3-4) and its part of
+                    // F[:, ei]' (P F[:, ej]); a DPP add joins the halves.  18 fp64 FMAs per lane and step
+                    // instead of 30 (the nz 7 unicycle: 28 entries, 56 lanes)
+#ifndef MPCG_FAC_PAIR
+#define MPCG_FAC_PAIR 0
+#endif
+                    constexpr bool PAIR_EL = MPCG_FAC_PAIR && FAC_FLAT && NU == 2 && NX == 5 && !C::COMPACT &&
+                                             !C::FCONST && !GFH && 2 * NT <= 64;
+                    constexpr int RH = PAIR_EL ? 3 : NX;  // cost-to-go rows per lane
+                    const int el = PAIR_EL ? (lane >> 1) : lane;  // the lane's block entry
+                    const int half = PAIR_EL ? (lane & 1) : 0;
+                    // the lane's rows of P F (half 1: rows 3, 4 and a dummy row 4 with a zero weight)
+                    auto prow = [&](int t) -> int { return PAIR_EL ? (half == 0 ? t : (t < 2 ? 3 + t : 4)) : t; };
+                    auto prow_on = [&](int t) -> bool { return !PAIR_EL || half == 0 || t < 2; };
                     // element lane -> (ei, ej), ei >= ej, of the nz x nz block
                     int ei = 0;
-                    while ((ei + 1) * (ei + 2) / 2 <= lane && ei < NZ - 1) ++ei;
-                    const int ej = lane < NT ? lane - ei * (ei + 1) / 2 : 0;
+                    while ((ei + 1) * (ei + 2) / 2 <= el && ei < NZ - 1) ++ei;
+                    const int ej = el < NT ? el - ei * (ei + 1) / 2 : 0;
                     // barrier entries of (ei, ej); DZ is the always-zero slot
                     const int dhd = (ei == ej) ? ei : DZ;
                     int dhb = DZ;
@@ -1575,10 +1596,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                     if (!FAC_FLAT && lane == 0) S.flag = 0;
                     wave_sync();
                     // prefetch of stage N-1's block
-                    const int le = lane < NT ? lane : 0;
+                    const int le = el < NT ? el : 0;
                     double fi[NX], fj[NX], hv;
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) { fi[m] = Fat(N - 1, m, ei); fj[m] = Fat(N - 1, m, ej); }
+                    for (int m = 0; m < NX; ++m) fj[m] = Fat(N - 1, m, ej);
+#pragma unroll
+                    for (int t = 0; t < RH; ++t) fi[t] = prow_on(t) ? Fat(N - 1, prow(t), ei) : 0.0;
                     // rows of [B A] that vary over the stages: with the constant rows (FCONST) only x+ and
                     // y+; the others stay in fi / fj from the fill above (their per-stage re-evaluation
                     // on the lane's runtime column compiled to branches inside the recursion)
@@ -1618,8 +1641,16 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
 #pragma unroll
                     for (int kk = N - 1; kk >= 0; --kk) {
                         double Pm[NP];
+                        if constexpr (PAIR_EL) {
+                            // the lane's rows of the cost-to-go (two distinct addresses per read)
 #pragma unroll
-                        for (int e = 0; e < NP; ++e) Pm[e] = S.P[kk + 1][e];
+                            for (int t = 0; t < RH; ++t)
+#pragma unroll
+                                for (int l = 0; l < NX; ++l) Pm[t * NX + l] = S.P[kk + 1][sym(prow(t), l)];
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < NP; ++e) Pm[e] = S.P[kk + 1][e];
+                        }
                         // prefetch of the next (lower) stage's block; it lands while this one is
                         // reduced.  FAC_FLAT: every lane runs one branch-free block, the five row
                         // products advance together, and the prefetch is issued after the pivot
@@ -1640,6 +1671,12 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                                 for (int m = 0; m < NFV; ++m)
                                     if (varies(m)) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
                                 hv2 = HelS() + S.dH[kn][dhd] + S.dH[kn][dhb];
+                            } else if constexpr (PAIR_EL) {
+#pragma unroll
+                                for (int m = 0; m < NX; ++m) fj2[m] = Fat(kn, m, ej);
+#pragma unroll
+                                for (int t = 0; t < RH; ++t) fi2[t] = prow_on(t) ? Fat(kn, prow(t), ei) : 0.0;
+                                hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
                             } else {
 #pragma unroll
                                 for (int m = 0; m < NFV; ++m)
@@ -1649,7 +1686,22 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         };
                         if constexpr (!FAC_FLAT) prefetch();
                         double v = hv;
-                        if constexpr (FAC_FLAT) {
+                        if constexpr (PAIR_EL) {
+                            // the lane's rows t of P F[:, ej], then its part of F[:, ei]' (P F[:, ej]) (half 1
+                            // starts from 0), the halves joined on the even lane (DPP row_shl:1)
+                            double tm[RH];
+#pragma unroll
+                            for (int t = 0; t < RH; ++t) tm[t] = 0.0;
+#pragma unroll
+                            for (int l = 0; l < NX; ++l)
+#pragma unroll
+                                for (int t = 0; t < RH; ++t) tm[t] += Pm[t * NX + l] * fj[l];
+                            v = half == 0 ? hv : 0.0;
+#pragma unroll
+                            for (int t = 0; t < RH; ++t) v += fi[t] * tm[t];
+                            v += dpp_d<0x101>(v);
+                            S.Msc[(el < NT && half == 0) ? el : 64 + lane] = v;
+                        } else if constexpr (FAC_FLAT) {
                             double tm[NX];
 #pragma unroll
                             for (int m = 0; m < NX; ++m) tm[m] = 0.0;
@@ -1677,9 +1729,10 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                           if (FAC_FLAT || lane < NP) {
                             // the pivot block (element lanes 0, 1, 2) straight from their registers:
                             // the recursion's critical path skips one LDS round trip
+                            constexpr int LS_ = PAIR_EL ? 2 : 1;  // lane stride of the block entries
                             const double m00 = FAC_FLAT ? readlane_d(v, 0) : S.Msc[0];
-                            const double m10 = FAC_FLAT ? readlane_d(v, 1) : S.Msc[1];
-                            const double m11 = FAC_FLAT ? readlane_d(v, 2) : S.Msc[2];
+                            const double m10 = FAC_FLAT ? readlane_d(v, LS_) : S.Msc[1];
+                            const double m11 = FAC_FLAT ? readlane_d(v, 2 * LS_) : S.Msc[2];
                             const double mi0 = S.Msc[sym(NU + pi_, 0)], mi1 = S.Msc[sym(NU + pi_, 1)];
                             const double mj0 = S.Msc[sym(NU + pj_, 0)], mj1 = S.Msc[sym(NU + pj_, 1)];
                             const double mij = S.Msc[sym(NU + pi_, NU + pj_)];
@@ -2458,14 +2511,17 @@ __global__ __launch_bounds__(64, 1) void sqp_kernel(mpcg_problem pr, int batch, 
                         alpha = 0.995 * amax;
                         if (alpha > 1.0) alpha = 1.0;
                         if (alpha >= 1e-12) {
-                            // rows move with the corrector step (rin, ddz of the current iterate)
+                            // rows move with the corrector step (rin, ddz of the current iterate), then
+                            // t and lambda are floored at qp_t_min (a compare-select: NaN passes through)
+                            const double tmin = pr.qp_t_min;
 #pragma unroll
                             for (int s = 0; s < C::SLOTS; ++s) {
                                 if (!active(s)) continue;
                                 double dt, dl;
                                 row_step(s, dt, dl);
-                                R.t[s] += alpha * dt;
-                                R.l[s] += alpha * dl;
+                                const double tn = R.t[s] + alpha * dt, ln = R.l[s] + alpha * dl;
+                                R.t[s] = tn < tmin ? tmin : tn;
+                                R.l[s] = ln < tmin ? tmin : ln;
                             }
                         }
                     }

@@ -55,10 +55,17 @@ def _row_nnz(lay):
 
 def ipm_iteration_ops(lay) -> int:
     """fp64 operations of one interior-point iteration over the whole horizon."""
+    return int(sum(ipm_iteration_ops_by_part(lay).values()))
+
+
+def ipm_iteration_ops_by_part(lay) -> dict:
+    """ipm_iteration_ops split by the algorithm's parts: residuals, barrier-augmented Hessian,
+    Riccati factorisation, the two Newton solves (gradient, vector passes, row steps) and the
+    centring + update (scripts/phase_isa.py sets them beside the kernel's phases)."""
     N, nu, nx = lay.N, lay.nu, lay.nx
     nz = nu + nx
     h = _row_nnz(lay)
-    total = 0
+    parts = {"residuals": 0, "barrier": 0, "factorisation": 0, "newton_solves": 0, "update": 0}
     for k in range(N):
         rows = [1] * (2 * nu) + ([1] * (2 * nx) + h if k >= 1 else [])
         m = len(rows)
@@ -82,10 +89,16 @@ def ipm_iteration_ops(lay) -> int:
         sol += sum(2 * c + 5 for c in rows) + 2 * m              # row steps, step length
         # centring + update
         upd = 8 * m + 2 * nz + 3 * nx
-        total += res + bar + fac + 2 * sol + upd
+        parts["residuals"] += res
+        parts["barrier"] += bar
+        parts["factorisation"] += fac
+        parts["newton_solves"] += 2 * sol
+        parts["update"] += upd
     # terminal stage: P_N = H_N, its part of the residuals and update
-    total += nx * (nx + 1) + 2 * nx + 2 * nz
-    return int(total)
+    parts["factorisation"] += nx * (nx + 1)
+    parts["residuals"] += 2 * nx
+    parts["update"] += 2 * nz
+    return parts
 
 
 def linearisation_ops(lay, rk_steps: int | None = None) -> int:

@@ -277,4 +277,8 @@ def config_layout(cfg: str) -> Layout:
         lay = ca_decomp_layout(N=30, max_constraints=12)
         lay.name = "C3"
         return lay
+    if cfg == "T10":
+        # diagnostic shape (not a BASELINE config): N 10, 2 obstacles -- the built-in test instance
+        # whose LDS block (17 KB) admits two waves per SIMD, for register-budget A/B runs
+        return tmpc_layout(N=10, max_obstacles=2, name="T10")
     raise KeyError(f"config {cfg} has no layout")

@@ -18,6 +18,8 @@ ABDIR = os.path.join(ROOT, "oscar_mpc_planner_mr_modification_amd", "build", "ab
 
 
 def lib(name):
+    if name == "prod":  # the production library
+        return os.path.join(ROOT, "oscar_mpc_planner_mr_modification_amd", "libmpcg.so")
     return os.path.join(ABDIR, name, "libmpcg.so")
 
 

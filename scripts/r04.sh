@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-4 GPU recipes, one named step per argument (each step under its own time limit; the
+# first failing step ends the call):
+#   bash scripts/r04.sh trace parity sqp tests smoke bench profile
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+tag=${R04_TAG:-r04}
+step() {  # step <name> <seconds> <output file> <command...>
+  local name=$1 secs=$2 out=$3; shift 3
+  echo "[$(date +%T)] $name -> $out"
+  timeout -k 10 $secs "$@" > "$out" 2>&1 || { echo "step $name failed ($?)"; tail -n 20 "$out"; exit 1; }
+}
+for s in "$@"; do
+  case $s in
+    trace)  # interior-point traces of the determined full-SQP divergences
+      T="python -u scripts/trace_solve.py"
+      step trace1 300 gpurun_out/${tag}_trace_c2_7414_sqp_full.log $T --config C2 --scenes 1024 --solve 7414 --lib-solve 7414 --solver-type SQP --variant full
+      step trace2 300 gpurun_out/${tag}_trace_c2_7414_rti_lean.log $T --config C2 --scenes 1024 --solve 7414 --lib-solve 7414 --solver-type SQP_RTI --variant lean
+      step trace3 300 gpurun_out/${tag}_trace_c4_6290_sqp_full.log $T --config C4 --scenes 2048 --solve 6290 --lib-solve 6290 --solver-type SQP --variant full ;;
+    parity)  # full-size parity of every config, product (lean) and FULL launches
+      step parity 1500 gpurun_out/${tag}_fullsize_parity.jsonl python -u scripts/parity_full.py --configs C2,C1,C3,C4,C5,C5B,JS,JD --ws 2 --warm-first 0 ;;
+    sqp)
+      step sqp 900 gpurun_out/${tag}_sqp_parity.jsonl python -u scripts/parity_full.py --configs C2,C1,C4 --ws 2 --warm-first 0 --solver-type SQP ;;
+    tests)
+      step tests 1500 gpurun_out/${tag}_gpu_tests.log python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ;;
+    smoke)
+      step smoke 300 gpurun_out/${tag}_smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      for c in ${R04_BENCH:-C2}; do
+        step bench_$c 600 gpurun_out/${tag}_bench_$(echo $c | tr A-Z a-z).json python -u bench.py --config $c --steps 20 --warmup 5
+      done ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo all-done
