@@ -102,6 +102,9 @@ typedef struct mpcg_problem {
                                       interior-point step (HPIPM's t_min / lam_min safeguard; 1e-12 here, where
                                       the dual-degenerate SH-MPC QPs' exit decisions stop depending on rounding,
                                       DESIGN.md §2.2); 0 = no floor */
+    double qp_mu_max;              /* divergence test: an interior point whose mean complementarity reaches this
+                                      (1e8: 1e8 x the cold start's) is diverging -- the QP is infeasible, its duals
+                                      blow up -- and ends with the NaN status */
 } mpcg_problem;
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,

@@ -608,7 +608,11 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
             if (KK) {
                 /* diagnostic kernel-forms build: (H dz + g) + (box + the h rows' sums per lane
                  * part folded part 0 + part 1 + part 2), then + F' pi term by term, - pi_prev */
-                const int parts = (64 / (N + 1)) >= 3 ? 3 : 2;
+#ifdef ORC_BICYCLE_CA
+                const int parts = 2; /* the kernel's bicycle instances run two parts (MPCG_PARTS_BIKE) */
+#else
+                const int parts = (64 / (N + 1)) >= 3 ? 3 : 2; /* Cfg::PARTS_MAX */
+#endif
                 double rh[3][NZ];
                 memset(rh, 0, sizeof rh);
                 for (int c = 0; c < S->ni; c++) {
@@ -918,8 +922,8 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
         double rs, re, ri, mu;
         int m;
         qp_residuals(w, &rs, &re, &ri, &mu, &m);
-        /* non-finite or diverged (infeasible QP: duals blow up) -> NaN status */
-        if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { status = AC_NAN; break; }
+        /* non-finite or diverged (infeasible QP: duals blow up; qp_mu_max) -> NaN status */
+        if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < pr->qp_mu_max)) { status = AC_NAN; break; }
         if (getenv("ORC_DEBUG")) fprintf(stderr, "  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", it, rs, re, ri, mu);
         if (getenv("ORC_DEBUG2")) {
             /* top complementarity contributors */

@@ -54,7 +54,7 @@ class OrcProblem(C.Structure):
         ("i_w_tangle", C.c_int), ("i_w_tcont", C.c_int), ("nu", C.c_int),
         ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
         ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
-        ("qp_t_min", C.c_double),
+        ("qp_t_min", C.c_double), ("qp_mu_max", C.c_double),
     ]
 
 
@@ -152,6 +152,8 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.nlp_tol = opts.get("nlp_tol", 1e-2)
     # floor of t and lambda after every interior-point step
     pr.qp_t_min = opts.get("qp_t_min", 1e-12)
+    # divergence test of the interior point
+    pr.qp_mu_max = opts.get("qp_mu_max", 1e8)
     return pr
 
 

@@ -390,6 +390,7 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->nlp_tol = 1e-2;
     // the interior point's t / lambda floor
     pr->qp_t_min = 1e-12;
+    pr->qp_mu_max = 1e8;
     return 0;
 }
 

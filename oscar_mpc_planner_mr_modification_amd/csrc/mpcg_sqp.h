@@ -158,7 +158,11 @@ struct Cfg {
     // parameter block instead of LDS, and their gaps are recomputed from the iterate:
     // only the ellipsoid rows keep gradients / gaps in LDS.  Used where it lowers the
     // LDS footprint below an occupancy step (C5: 51.6 -> 36.6 KB, 3 -> 4 solves per CU).
+#ifdef MPCG_LIN_PARAMS_ALL
+    static constexpr bool LIN_PARAMS = true;  // occupancy experiments: the compact row storage everywhere
+#else
     static constexpr bool LIN_PARAMS = NS > 0 || N >= 30;
+#endif
     // gradient components kept per LDS row: with LIN_PARAMS the psi component is
     // rebuilt from (x, y) components and the stage's disc-offset derivatives
     static constexpr int DGC = LIN_PARAMS ? 2 : 3;
@@ -304,9 +308,18 @@ struct Lds {
 };
 
 // four solves per CU need at most a quarter of the CU's 160 KiB of LDS per workgroup
+// (MPCG_LDS_SOLVES_PER_CU, occupancy experiments only: another LDS line -- 8 for two waves per SIMD
+// -- and the smallest storage that gets under it)
+#ifdef MPCG_LDS_SOLVES_PER_CU
+constexpr size_t LDS_QUARTER = 160 * 1024 / MPCG_LDS_SOLVES_PER_CU;
+constexpr bool LDS_SMALLEST = true;
+#else
 constexpr size_t LDS_QUARTER = 160 * 1024 / 4;
+constexpr bool LDS_SMALLEST = false;
+#endif
 template <class C>
 __host__ __device__ constexpr bool lds_lean() {
+    if (LDS_SMALLEST) return C::COMPACT || sizeof(Lds<C, false>) > LDS_QUARTER;
     return C::COMPACT || (sizeof(Lds<C, false>) > LDS_QUARTER && sizeof(Lds<C, true>) <= LDS_QUARTER);
 }
 template <class C>
@@ -314,6 +327,7 @@ __host__ __device__ constexpr bool lds_gfh() {
 #ifdef MPCG_NO_GFH
     return false;
 #else
+    if (LDS_SMALLEST) return sizeof(Lds<C, lds_lean<C>(), false>) > LDS_QUARTER;
     return sizeof(Lds<C, lds_lean<C>(), false>) > LDS_QUARTER && sizeof(Lds<C, lds_lean<C>(), true>) <= LDS_QUARTER;
 #endif
 }
@@ -1445,7 +1459,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
             if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0)
                 printf("[%d]  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", sol, qit, rs, re, ri, mu);
 #endif
-            if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < 1e16)) { qstat = AC_NAN; break; }
+            if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < pr.qp_mu_max)) { qstat = AC_NAN; break; }
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
             wave_sync();

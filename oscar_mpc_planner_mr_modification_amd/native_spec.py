@@ -40,7 +40,7 @@ class MpcgProblem(C.Structure):
         # ABI 6
         ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
         # ABI 7
-        ("qp_t_min", C.c_double),
+        ("qp_t_min", C.c_double), ("qp_mu_max", C.c_double),
     ]
 
 
@@ -50,7 +50,7 @@ class MpcgProblem(C.Structure):
 # later QPs of a full SQP call (solver_type="SQP") warm (DESIGN.md §2 "QP start")
 DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2,
                        qp_warm_start=2, qp_ws_thr=0.1, qp_warm_first=0, solver_type="SQP_RTI", nlp_max_iter=100,
-                       nlp_tol=1e-2, qp_t_min=1e-12)
+                       nlp_tol=1e-2, qp_t_min=1e-12, qp_mu_max=1e8)
 NLP_SOLVER = {"SQP_RTI": 0, "SQP": 1}
 # ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
 UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
@@ -90,6 +90,7 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.nlp_max_iter = o["nlp_max_iter"]
     pr.nlp_tol = o["nlp_tol"]
     pr.qp_t_min = o["qp_t_min"]
+    pr.qp_mu_max = o["qp_mu_max"]
     return pr
 
 

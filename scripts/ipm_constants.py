@@ -5,7 +5,9 @@ on the bench batches, with the oracle (test infrastructure):
    the copies on which the two kernel-agnostic oracle builds (HPIPM forms, literal forms)
    part, and those on which the kernel-forms build ends like neither;
 2. what the chosen floor does elsewhere (exit agreement and max |dx| against no floor);
-3. the cold-start constants qp_mu0 / qp_thr0 (HPIPM's thr0 is 0.1).
+3. the cold-start constants qp_mu0 / qp_thr0 (HPIPM's thr0 is 0.1);
+4. the interior point's divergence test qp_mu_max in full SQP (rounding-decided solves) and in
+   SQP-RTI (what it changes against round 3's 1e16).
 
     python scripts/ipm_constants.py > profiles/r04_ipm_constants.txt
 """
@@ -62,6 +64,23 @@ def main():
         lay, b = inputs(cfg, S)
         for mu0, thr0 in ((1.0, 1.0), (1.0, 0.1), (10.0, 0.1), (10.0, 1.0)):
             print(f"{cfg} mu0 {mu0:g} thr0 {thr0:g}: {summary(run(lay, b, qp_mu0=mu0, qp_thr0=thr0))}", flush=True)
+    print("\n# 4. divergence test qp_mu_max: full SQP rounding-decided solves (HPIPM vs literal forms), SQP-RTI changes")
+    for cfg, S in (("C4", 2048), ("C2", 1024)):
+        lay, b = inputs(cfg, S)
+        for mmax in (1e16, 1e10, 1e8):
+            a = run(lay, b, solver_type="SQP", qp_mu_max=mmax)
+            c = run(lay, b, "literal", solver_type="SQP", qp_mu_max=mmax)
+            dec = parted(a, c)
+            print(f"{cfg} SQP qp_mu_max {mmax:g}: rounding-decided {int(dec.sum())} (exit-decided "
+                  f"{int((a['status'] != c['status']).sum())}) | {summary(a)}", flush=True)
+    for cfg, S in (("C2", 1024), ("C4", 2048), ("C5", 2048), ("C5B", 2048), ("C1", 1024)):
+        lay, b = inputs(cfg, S)
+        a, c = run(lay, b, qp_mu_max=1e16), run(lay, b, qp_mu_max=1e8)
+        same = a["status"] == c["status"]
+        ok = same & (a["status"] == 1)
+        dx = np.abs(a["xtraj"] - c["xtraj"]).reshape(len(same), -1)[ok].max() if ok.any() else 0.0
+        print(f"{cfg} SQP-RTI qp_mu_max 1e16 -> 1e8: exit changes {int((~same).sum())}, max |dx| of successful "
+              f"{dx:.2e}, ipm/solve {a['qp_iter'].mean():.3f} -> {c['qp_iter'].mean():.3f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -84,7 +84,11 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     bad = same & (got["exit"] != 1)
     dx = np.abs(got["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
     st = np.stack([ref["res_stat"], ref["res_eq"], ref["res_ineq"], ref["res_comp"]], 1)
-    st_rel = (np.abs(got["stats"] - st) / np.maximum(1.0, np.abs(st)))[same].max() if same.any() else 0.0
+    st_relv = (np.abs(got["stats"] - st) / np.maximum(1.0, np.abs(st))).max(1)
+    # the NLP residuals of solves in which no QP stopped at the cap (a capped QP's unconverged step
+    # moves the final linearisation point, see capfree below)
+    capfree0 = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
+    st_rel = st_relv[same & capfree0].max() if (same & capfree0).any() else 0.0
     dis = np.flatnonzero(~same)
     # failed solves that took the same path on both sides (same RTI and IPM iteration counts) with
     # every accepted step from a converged QP
@@ -111,6 +115,8 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     dxk = np.abs(got["xtraj"] - kf["xtraj"]).reshape(len(same), -1).max(1)
     same_k = got["exit"] == kf["status"]
     capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
+    # successful solves more than 1e-4 apart although no QP of either side stopped at the cap
+    over_capfree = ok & (dx > 1e-4) & capfree
     return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "solver_type": solver_type,
             "oracle": "literal" if literal else "default (HPIPM forms)", "gpu_variant": variant, **lean_full,
             "kernel_forms_exit_agreement": float(same_k.mean()),
@@ -151,7 +157,9 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
             # point stood; with the warm start and in full SQP the next QPs start from it)
             "capfree_frac": float(capfree.mean()),
             "capfree_exit_agreement": float(same[capfree].mean()) if capfree.any() else None,
-            "capfree_max_abs_dx_success": float(dx[capfree & ok].max()) if (capfree & ok).any() else None}
+            "capfree_max_abs_dx_success": float(dx[capfree & ok].max()) if (capfree & ok).any() else None,
+            "n_success_dx_over_1e-4_capfree": int(over_capfree.sum()),
+            "n_success_dx_over_1e-4_capped": int((ok & (dx > 1e-4) & ~capfree).sum())}
 
 
 def main():

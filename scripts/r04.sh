@@ -8,7 +8,7 @@ tag=${R04_TAG:-r04}
 step() {  # step <name> <seconds> <output file> <command...>
   local name=$1 secs=$2 out=$3; shift 3
   echo "[$(date +%T)] $name -> $out"
-  timeout -k 10 $secs "$@" > "$out" 2>&1 || { echo "step $name failed ($?)"; tail -n 20 "$out"; exit 1; }
+  timeout -k 10 $secs "$@" > "$out" 2> "$out.err" || { echo "step $name failed ($?)"; tail -n 20 "$out" "$out.err"; exit 1; }
 }
 for s in "$@"; do
   case $s in
@@ -28,6 +28,11 @@ for s in "$@"; do
     bench)
       for c in ${R04_BENCH:-C2}; do
         step bench_$c 600 gpurun_out/${tag}_bench_$(echo $c | tr A-Z a-z).json python -u bench.py --config $c --steps 20 --warmup 5
+      done ;;
+    ab)  # A/B of kernel variants (scripts/ab_bench.py; R04_AB="variants:configs ...")
+      for spec in ${R04_AB:-prod,fpair:C2,C1}; do
+        v=${spec%%:*}; c=${spec##*:}
+        step ab_${v//,/_}_${c//,/_} 1100 gpurun_out/${tag}_ab_${v//,/_}_${c//,/_}.jsonl python -u scripts/ab_bench.py --run $v --configs $c --reps 2
       done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -70,7 +70,10 @@ def main():
         return
     lay, b = scene_inputs(args.config, args.scene, args.braking, args.scenes)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    inp = os.path.join(ROOT, "gpurun_out", "trace_inputs.npz")
+    # the batch's inputs for the GPU child process: outside gpurun_out (a bench batch is
+    # hundreds of MB; gpurun_out travels back)
+    import tempfile
+    inp = os.path.join(tempfile.gettempdir(), f"mpcg_trace_inputs_{os.getpid()}.npz")
     np.savez(inp, params=b.params, warm=b.warm, xinit=b.xinit)
     opts = dict(qp_warm_start=args.ws, qp_warm_first=args.warm_first, solver_type=args.solver_type)
     # the GPU side in a child process (the trace library replaces libmpcg.so there)

@@ -5,16 +5,21 @@ plan, C3 4096 bicycle solves, JS (the shipped jackalsimulator solver) 4096 x 5, 
 shipped jackal / dingo solver, N 30 with 5 obstacles) 4096 x 5, C1 1024 scenes; the
 reference's QP start (qp_solver_warm_start 2, warm_start_first_qp off).
 
-Every solve is compared with the oracle's default build, and the oracle's literal-forms
-build (the same algorithm, another legal rounding: oracle/mpcg_oracle.c "Arithmetic forms")
-tells which solves rounding decides.  On every solve the two builds agree on (exit code,
-and successful trajectories within 1e-4 of each other) the GPU must have the same exit
-code and, if successful, a trajectory within 1e-4 (north_star); so must failed solves that
-took the same path.  A solve on which the two oracle builds part is rounding-decided --
-the divergence is in the problem, not in one implementation -- and the GPU must end there
-like one of the two builds.  Only the SH-MPC slack QPs have such solves (dual-degenerate,
-DESIGN.md §3.2: the interior point's exit reads residuals made of cancelling multipliers of
-1e13 and more); every other config is held to the default build on every solve."""
+The product launch -- the lean kernel variant that bench.py and mpcg_solve_batch_device run
+-- is compared with the oracle's default build (HPIPM's arithmetic forms) on every solve:
+identical exit codes and, for successful solves, trajectories within 1e-4 (north_star) --
+except where a QP of the solve stopped at the 50-iteration cap on both sides: the RTI loop
+then ends on that QP's unconverged step, which is wherever the stalled interior point stood
+(DESIGN.md §2 "QP start"), so only the exit code is held there (C5B: 1 of 8,192 copies).  The
+FULL kernel variant (stats buffer: the NLP residuals of the drop-in's AcadosInfo) must end
+every solve like the lean one.  The literal-forms oracle build tells which solves rounding
+decides; with the interior point's t / lambda floor no bench batch has one.
+
+solver_type SQP (one full acados SQP call per solve, the FULL variant): C2 and C4 at bench
+size, with the same bar on every solve whose QPs all converged on both sides; a solve in
+which some QP stopped at the 50-iteration cap applies that QP's unconverged step and carries
+it into the next, warm-started QP, so its path is set by where the stalled interior point
+stood (DESIGN.md §2 "QP start").  Those solves must still end with the same exit code."""
 import os
 import sys
 
@@ -33,17 +38,37 @@ def test_fullsize_parity(cfg):
 
     r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0)
     print({k: v for k, v in r.items() if k != "rounding_decided"})
-    print("rounding-decided solves:", r["rounding_decided"])
-    assert r["determined_exit_agreement"] == 1.0, r["disagreeing"]
-    assert r["determined_max_abs_dx_success"] <= 1e-4, r["success_dx_over_1e-4"]
+    # the kernel the bench times
+    assert r["gpu_variant"] == "lean"
+    # no rounding-decided solve: the default build decides every exit and every trajectory
+    assert r["n_rounding_decided"] == 0, r["rounding_decided"]
+    assert r["exit_agreement"] == 1.0, r["disagreeing"]
+    assert r["n_success_dx_over_1e-4_capfree"] == 0, r["success_dx_over_1e-4"]
+    assert r["capfree_max_abs_dx_success"] <= 1e-4
+    assert r["n_success_dx_over_1e-4_capped"] <= 0.001 * r["solves"], r["success_dx_over_1e-4"]
     assert r["same_path_failed_dx"] is None or r["same_path_failed_dx"] <= 1e-4
-    assert r["rounding_decided_end_like_a_build"], r["rounding_decided"]
-    floor = {"C5": 0.85, "C5B": 0.55}.get(cfg, 0.9)
+    # the FULL variant ends every solve like the lean one
+    assert r["lean_full_exit_equal"] and r["lean_full_info_equal"], r
+    assert r["lean_full_max_abs_dx"] <= 1e-9, r["lean_full_max_abs_dx"]
+    # the NLP residuals of the FULL variant against the oracle's
+    assert r["stats_max_rel_diff"] <= 1e-6, r["stats_max_rel_diff"]
+    floor = {"C5": 0.85, "C5B": 0.7}.get(cfg, 0.9)
     assert r["success_frac"] >= floor, r["success_frac"]
-    if cfg in ("C5", "C5B"):
-        assert r["n_rounding_decided"] <= 0.005 * r["solves"], r["n_rounding_decided"]
-    else:
-        # no rounding-decided solve: the default build decides every exit and every trajectory
-        assert r["n_rounding_decided"] == 0, r["rounding_decided"]
-        assert r["exit_agreement"] == 1.0 and r["max_abs_dx_success"] <= 1e-4
+    if cfg not in ("C5", "C5B"):
         assert r["rti_iters_per_solve"] >= 9.0
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_fullsize_parity_full_sqp(cfg):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from parity_full import DEFAULT_SCENES, compare
+
+    r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0, solver_type="SQP")
+    print({k: v for k, v in r.items() if k != "rounding_decided"})
+    assert r["gpu_variant"] == "full"
+    assert r["n_rounding_decided"] == 0, r["rounding_decided"]
+    assert r["exit_agreement"] == 1.0, r["disagreeing"]
+    assert r["n_success_dx_over_1e-4_capfree"] == 0, r["success_dx_over_1e-4"]
+    assert r["capfree_max_abs_dx_success"] <= 1e-4
+    assert r["capfree_frac"] >= 0.95
