@@ -843,6 +843,8 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
     if (lane < NU) S.z[N][lane] = 0.0;
     wave_sync();
 
+    // the interior point's divergence test and t / lambda floor, read once
+    const double mu_max = pr.qp_mu_max, tmin = pr.qp_t_min;
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0, n_maxit = 0;
     double res_eq = 0.0;
     double nlp_stat = 0.0, nlp_ineq = 0.0, nlp_comp = 0.0;  // NLP residuals of the last linearisation
@@ -1459,7 +1461,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
             if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0)
                 printf("[%d]  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", sol, qit, rs, re, ri, mu);
 #endif
-            if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < pr.qp_mu_max)) { qstat = AC_NAN; break; }
+            if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < mu_max)) { qstat = AC_NAN; break; }
             if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
             if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
             wave_sync();
@@ -2493,14 +2495,38 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                         dl = -(rc + l * dt) * R.it(s);
                     };
                     // step to the boundary: min over rows of -t/dt and -l/dl = 1 / max(-dt/t, -dl/l)
+                    // STEP_FORMS: in the predictor rc = l t, so dl = -l (t + dt) / t and a row's
+                    // multiplier blocks (dl < 0) exactly when t + dt > 0, at -dl / l = 1 + dt / t: the row's
+                    // bound is max(-dt/t, 1 + dt/t) (the second term is <= 0 < the first when it does not
+                    // block), no reciprocal of l and no branch; in the corrector the branch on dl < 0 is a
+                    // select (the wave computes the reciprocal whenever any lane needs it)
+#ifndef MPCG_STEP_FORMS
+#define MPCG_STEP_FORMS 1
+#endif
                     double rmax = 0.0;
+                    if (MPCG_STEP_FORMS && ph == 0) {
 #pragma unroll
-                    for (int s = 0; s < C::SLOTS; ++s) {
-                        if (!active(s)) continue;
-                        double dt, dl;
-                        row_step(s, dt, dl);
-                        rmax = fmax(rmax, -dt * R.it(s));
-                        if (dl < 0.0) rmax = fmax(rmax, -dl * frcp(R.l[s]));
+                        for (int s = 0; s < C::SLOTS; ++s) {
+                            if (!active(s)) continue;
+                            double dt, dl;
+                            row_step(s, dt, dl);
+                            const double x = dt * R.it(s);
+                            rmax = fmax(rmax, fmax(-x, 1.0 + x));
+                        }
+                    } else {
+#pragma unroll
+                        for (int s = 0; s < C::SLOTS; ++s) {
+                            if (!active(s)) continue;
+                            double dt, dl;
+                            row_step(s, dt, dl);
+                            rmax = fmax(rmax, -dt * R.it(s));
+                            if (MPCG_STEP_FORMS) {
+                                const double c = -dl * frcp(R.l[s]);
+                                rmax = fmax(rmax, dl < 0.0 ? c : 0.0);
+                            } else if (dl < 0.0) {
+                                rmax = fmax(rmax, -dl * frcp(R.l[s]));
+                            }
+                        }
                     }
                     rmax = wave_max(rmax);
                     const double amax = rmax > 0.0 ? frcp(rmax) : 1e300;
@@ -2527,7 +2553,6 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                         if (alpha >= 1e-12) {
                             // rows move with the corrector step (rin, ddz of the current iterate), then
                             // t and lambda are floored at qp_t_min (a compare-select: NaN passes through)
-                            const double tmin = pr.qp_t_min;
 #pragma unroll
                             for (int s = 0; s < C::SLOTS; ++s) {
                                 if (!active(s)) continue;
