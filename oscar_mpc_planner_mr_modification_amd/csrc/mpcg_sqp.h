@@ -2315,9 +2315,14 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                     }
                     STAMP_LAP(6);
                     // each chain step's value is recorded in LDS by the lane that owns it (a
-                    // predicated store off the VALU path) and read back after the chain; the
-                    // register-starved bicycle instance selects it into registers instead
-                    constexpr bool CHAIN_REC = !C::COMPACT;
+                    // predicated store off the VALU path) and read back after the chain.  The
+                    // register-starved bicycle instance did the selects into registers until round 4;
+                    // the records keep six doubles per chain out of its registers: scratch 560 -> 504
+                    // B/lane, C3 19.50 -> 18.99 ms (profiles/r04i_ab_*; MPCG_C3_CHAIN_REC=0: A/B)
+#ifndef MPCG_C3_CHAIN_REC
+#define MPCG_C3_CHAIN_REC 1
+#endif
+                    constexpr bool CHAIN_REC = !C::COMPACT || MPCG_C3_CHAIN_REC;
                     double pu[NX], pmine[NX];
                     double* const pch = &S.bx[0][0];
                     static_assert((N + 1) * NZ >= N * NX, "chain storage");
