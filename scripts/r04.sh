@@ -29,6 +29,14 @@ for s in "$@"; do
       for c in ${R04_BENCH:-C2}; do
         step bench_$c 600 gpurun_out/${tag}_bench_$(echo $c | tr A-Z a-z).json python -u bench.py --config $c --steps 20 --warmup 5
       done ;;
+    latency)  # one Solver::solve() / one GuidanceConstraints::optimize through the drop-in's context
+      step latency_js 300 gpurun_out/${tag}_latency_js.json python -u scripts/latency.py --config JS --guesses 5
+      step latency_c2 300 gpurun_out/${tag}_latency_c2.json python -u scripts/latency.py --config C2 --guesses 8 ;;
+    profile)  # rocprofv3 kernel trace + PMC passes of the bench workloads (R04_PROF="C2 C1 ...")
+      for c in ${R04_PROF:-C2}; do
+        lc=$(echo $c | tr A-Z a-z)
+        step prof_$c 600 gpurun_out/${tag}_${lc}_prof.log bash scripts/profile_kernels.sh ${tag}_${lc} --config $c
+      done ;;
     ab)  # A/B of kernel variants (scripts/ab_bench.py; R04_AB="variants:configs ...")
       for spec in ${R04_AB:-prod,fpair:C2,C1}; do
         v=${spec%%:*}; c=${spec##*:}
