@@ -458,6 +458,30 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 
+// One step of a split vector chain: h + G . v.  MPCG_CHAIN_TREE: two partial sums (the first
+// half of the terms from h, the second from 0) joined by one add, so the step's dependent chain is
+// ceil(n/2) + 1 operations deep instead of n (the chains are latency-bound at one wave per SIMD)
+#ifndef MPCG_CHAIN_TREE
+#define MPCG_CHAIN_TREE 0
+#endif
+template <int n>
+__device__ __forceinline__ double chain_dot(double h, const double* G, const double* v) {
+    if constexpr (MPCG_CHAIN_TREE) {
+        constexpr int m = (n + 1) / 2;
+        double a = h, b = G[m] * v[m];
+#pragma unroll
+        for (int j = 0; j < m; ++j) a += G[j] * v[j];
+#pragma unroll
+        for (int j = m + 1; j < n; ++j) b += G[j] * v[j];
+        return a + b;
+    } else {
+        double a = h;
+#pragma unroll
+        for (int j = 0; j < n; ++j) a += G[j] * v[j];
+        return a;
+    }
+}
+
 // barrier contribution at (i, j), i >= j: diagonal part dh[0..nz) plus the
 // h-row block dh[nz..nz + NBT)
 template <class C>
@@ -2032,10 +2056,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                         double pn[RS];
 #pragma unroll
                         for (int t = 0; t < RS; ++t) {
-                            double a = hr[t];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += Gr[t][j] * pu[j];
-                            pn[t] = a;
+                            pn[t] = chain_dot<NX>(hr[t], Gr[t], pu);
                         }
                         if constexpr (C::REC_FLAT) {
                             // branch-free record: lanes that do not own the step write to the
@@ -2133,10 +2154,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                         double dn[RS];
 #pragma unroll
                         for (int t = 0; t < RS; ++t) {
-                            double a = ec[t];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += Gc[t][j] * dxu[j];
-                            dn[t] = a;
+                            dn[t] = chain_dot<NX>(ec[t], Gc[t], dxu);
                         }
                         if constexpr (C::REC_FLAT) {
 #ifndef MPCG_REC_SELECT
