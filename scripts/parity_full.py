@@ -85,10 +85,12 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     dx = np.abs(got["xtraj"] - ref["xtraj"]).reshape(len(same), -1).max(1)
     st = np.stack([ref["res_stat"], ref["res_eq"], ref["res_ineq"], ref["res_comp"]], 1)
     st_relv = (np.abs(got["stats"] - st) / np.maximum(1.0, np.abs(st))).max(1)
-    # the NLP residuals of solves in which no QP stopped at the cap (a capped QP's unconverged step
-    # moves the final linearisation point, see capfree below)
-    capfree0 = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
-    st_rel = st_relv[same & capfree0].max() if (same & capfree0).any() else 0.0
+    # solves in which no QP stopped at the 50-iteration cap on either side: every applied step is a
+    # converged QP solution (a capped QP's step is wherever its stalled interior point stood; with the
+    # warm start and in full SQP the next QPs start from it)
+    capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
+    # the NLP residuals of those solves (a capped step moves the final linearisation point)
+    st_rel = st_relv[same & capfree].max() if (same & capfree).any() else 0.0
     dis = np.flatnonzero(~same)
     # failed solves that took the same path on both sides (same RTI and IPM iteration counts) with
     # every accepted step from a converged QP
@@ -114,7 +116,6 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     kf = oracle_py.Oracle(lay, forms="kernel", **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=16)
     dxk = np.abs(got["xtraj"] - kf["xtraj"]).reshape(len(same), -1).max(1)
     same_k = got["exit"] == kf["status"]
-    capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
     # successful solves more than 1e-4 apart although no QP of either side stopped at the cap
     over_capfree = ok & (dx > 1e-4) & capfree
     return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "solver_type": solver_type,
