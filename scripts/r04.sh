@@ -18,7 +18,7 @@ for s in "$@"; do
       step trace2 300 gpurun_out/${tag}_trace_c2_7414_rti_lean.log $T --config C2 --scenes 1024 --solve 7414 --lib-solve 7414 --solver-type SQP_RTI --variant lean
       step trace3 300 gpurun_out/${tag}_trace_c4_6290_sqp_full.log $T --config C4 --scenes 2048 --solve 6290 --lib-solve 6290 --solver-type SQP --variant full ;;
     parity)  # full-size parity of every config, product (lean) and FULL launches
-      step parity 1500 gpurun_out/${tag}_fullsize_parity.jsonl python -u scripts/parity_full.py --configs C2,C1,C3,C4,C5,C5B,JS,JD --ws 2 --warm-first 0 ;;
+      step parity 1500 gpurun_out/${tag}_fullsize_parity.jsonl python -u scripts/parity_full.py --configs ${R04_PARITY:-C2,C1,C3,C4,C5,C5B,JS,JD} --ws 2 --warm-first 0 ;;
     ws)  # the restated warm start on every QP (qp_warm_first 1), full size
       step ws 900 gpurun_out/${tag}_ws_parity.jsonl python -u scripts/parity_full.py --configs C2,C4,C5 --ws 2 --warm-first 1 ;;
     sqp)
