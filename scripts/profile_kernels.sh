@@ -24,4 +24,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES \
   -d $o/prof_${tag}_lanes -o run --output-format csv \
   -- python3 bench.py --no-cpu --steps 3 --warmup 1 $extra > $o/prof_${tag}_lanes.log 2>&1
+# the effective clock under load (GRBM_GUI_ACTIVE / 8 XCDs / kernel time) and wave cycles: how much
+# of the launch the SIMDs are busy (the tail)
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+  -d $o/prof_${tag}_clk -o run --output-format csv \
+  -- python3 bench.py --no-cpu --steps 3 --warmup 1 $extra > $o/prof_${tag}_clk.log 2>&1
 echo profile-done
