@@ -18,9 +18,12 @@
 
 extern "C" {
 /* launcher of one compiled instance: enqueues the solve of `batch` problems on `stream`
- * and returns the hipError_t of the launch.  `workspace`: device memory of at least
- * batch x the instance's workspace bytes per solve on the stream's device (instances whose
- * stage blocks do not fit the LDS budget keep them there), or NULL when it needs none */
+ * and returns the hipError_t of the launch.  `workspace`: device memory on the stream's device
+ * of at least MPCG_QUEUE_BYTES + batch x the instance's workspace bytes per solve (instances
+ * whose stage blocks do not fit the LDS budget keep them there), whose first MPCG_QUEUE_BYTES
+ * are zero before the first launch on it (the work queue of sqp_kernel, which every launch
+ * leaves zeroed); or NULL for an instance without stage-block workspace (then one workgroup
+ * per problem, no queue) */
 typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream,
                                     unsigned long long* stamps, void* workspace);
 /* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher, the
@@ -29,8 +32,30 @@ typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpc
 int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
                            int qp_mem_size, long long workspace_bytes_per_solve, const char* traits);
 }
+/* the work-queue words at the head of an instance workspace (sqp_kernel) */
+#define MPCG_QUEUE_BYTES 256
 
 namespace mpcg {
+
+// grid of a work-queue launch: the workgroups the device holds at once (occupancy x CUs),
+// at most one per problem.  MPCG_QUEUE_GRID_PER_CU (A/B only) sets the workgroups per CU.
+template <class C, bool FULL>
+int queue_grid(int batch) {
+    static const int resident = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return 0;
+#ifdef MPCG_QUEUE_GRID_PER_CU
+        per_cu = MPCG_QUEUE_GRID_PER_CU;
+#else
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL>, 64, 0) != hipSuccess) return 0;
+#endif
+        return per_cu > 0 ? per_cu * cus : 0;
+    }();
+    // (no occupancy answer: one workgroup per problem, still through the queue)
+    return resident > 0 && resident < batch ? resident : batch;
+}
 
 template <class C>
 int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps,
@@ -38,14 +63,15 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
     // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
     // the full variant only when the call needs QP memory, the warm start, the residuals or
     // the full SQP
-    double* gws = (double*)workspace;
-    if (gfh_doubles<C>() > 0 && !gws) return (int)hipErrorInvalidValue;
+    if (gfh_doubles<C>() > 0 && !workspace) return (int)hipErrorInvalidValue;
+    unsigned* queue = C::QUEUE ? (unsigned*)workspace : nullptr;
+    double* gws = workspace ? (double*)((char*)workspace + MPCG_QUEUE_BYTES) : nullptr;
     if (io->stats || io->qp_in || io->qp_out || needs_full(*pr))
-        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
-                           stamps, gws);
+        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(queue ? queue_grid<C, true>(batch) : batch), dim3(64), 0,
+                           (hipStream_t)stream, *pr, batch, *io, stamps, gws, queue);
     else
-        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(batch), dim3(64), 0, (hipStream_t)stream, *pr, batch, *io,
-                           stamps, gws);
+        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(queue ? queue_grid<C, false>(batch) : batch), dim3(64), 0,
+                           (hipStream_t)stream, *pr, batch, *io, stamps, gws, queue);
     return (int)hipGetLastError();
 }
 

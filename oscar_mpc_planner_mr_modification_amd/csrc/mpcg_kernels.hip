@@ -162,8 +162,8 @@ static int stream_device(hipStream_t stream, int* dev) {
 
 static int launch_on_stream(const Inst& in, const mpcg_problem& pr, int batch, const mpcg_io& io,
                             hipStream_t stream) {
-    if (in.ws <= 0) return launch(in, pr, batch, io, stream, nullptr);
-    const size_t bytes = (size_t)batch * (size_t)in.ws;
+    // the work-queue words (mpcg_instance.h) then the stage blocks of GFH instances
+    const size_t bytes = MPCG_QUEUE_BYTES + (size_t)batch * (size_t)(in.ws > 0 ? in.ws : 0);
     int dev = 0;
     if (stream_device(stream, &dev)) { g_err = "mpcg_solve: no device for the stream"; return -1; }
     std::lock_guard<std::mutex> l(g_ws_mutex);
@@ -185,6 +185,11 @@ static int launch_on_stream(const Inst& in, const mpcg_problem& pr, int batch, c
             w->size = 0;
         }
         if (ok && hipMalloc(&w->ptr, bytes) != hipSuccess) { w->ptr = nullptr; ok = false; }
+        if (ok && hipMemsetAsync(w->ptr, 0, MPCG_QUEUE_BYTES, stream) != hipSuccess) {
+            (void)hipFree(w->ptr);
+            w->ptr = nullptr;
+            ok = false;
+        }
         (void)hipSetDevice(cur);
         if (!ok) { g_err = "mpcg_solve: workspace allocation failed"; return -1; }
         w->size = bytes;
@@ -240,7 +245,7 @@ struct mpcg_context {
     mpcg::Inst inst;
     int max_batch = 0;
     hipStream_t stream = nullptr;
-    void* ws = nullptr;      // the instance's workspace for max_batch solves (on the context's device)
+    void* ws = nullptr;      // work-queue words + the instance's workspace for max_batch solves (context's device)
     double* dev = nullptr;   // params | warm | xinit | lam_in | qp_in | xtraj | utraj | pobj | lam_out | qp_out | stats
     double* host = nullptr;  // pinned mirror of the same layout
     int* idev = nullptr;     // exit | info
@@ -463,7 +468,9 @@ mpcg_context* mpcg_context_create(const mpcg_problem* pr, int max_batch) {
               hipHostMalloc(&c->host, c->n_dbl * sizeof(double), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->idev, c->n_int * sizeof(int)) == hipSuccess &&
               hipHostMalloc(&c->ihost, c->n_int * sizeof(int), hipHostMallocDefault) == hipSuccess &&
-              (in.ws <= 0 || hipMalloc(&c->ws, (size_t)max_batch * (size_t)in.ws) == hipSuccess);
+              hipMalloc(&c->ws, MPCG_QUEUE_BYTES + (size_t)max_batch * (size_t)(in.ws > 0 ? in.ws : 0)) ==
+                  hipSuccess &&
+              hipMemset(c->ws, 0, MPCG_QUEUE_BYTES) == hipSuccess;
     if (!ok) {
         mpcg::g_err = "mpcg_context_create: device allocation failed";
         mpcg_context_destroy(c);

@@ -122,6 +122,17 @@ struct Cfg {
     static constexpr int PARTS = MODEL_ == 1 ? (MPCG_PARTS_BIKE < PARTS_MAX ? MPCG_PARTS_BIKE : PARTS_MAX) : PARTS_MAX;
     static_assert((N + 1) * PARTS <= 64, "horizon too long for one wavefront");
     static_assert(NTRI <= 64, "stage block larger than a wavefront");
+    // work-queue launch (sqp_kernel): the N <= 20 three-part unicycle instances (C1, C2, C5).  On the
+    // long horizons the loop around the solve moves the register allocation into scratch (C4 132 ->
+    // 840 B/lane, 44.3 -> 71.3 ms; JS / JD 0 -> 456 / 528 B/lane, C3 552 -> 720), so they keep one
+    // workgroup per problem (MPCG_QUEUE_ALL / MPCG_NO_QUEUE: A/B)
+#if defined(MPCG_NO_QUEUE)
+    static constexpr bool QUEUE = false;
+#elif defined(MPCG_QUEUE_ALL)
+    static constexpr bool QUEUE = true;
+#else
+    static constexpr bool QUEUE = MODEL_ == 0 && PARTS_MAX == 3;
+#endif
     // rows of a lane: box slots j (variable part + PARTS j, lower and upper
     // side: slots 2j, 2j + 1), then h slots r (h row part + PARTS r)
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
@@ -641,10 +652,11 @@ __host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
 #else
 #define MPCG_KERNEL_ATTR __launch_bounds__(64, 1)
 #endif
-template <class C, bool FULL = false>
-__global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
-                                                    unsigned long long* __restrict__ stamps,
-                                                    double* __restrict__ gws) {
+// one solve `sol` on the calling wavefront (the body of sqp_kernel)
+template <class C, bool FULL>
+__device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io,
+                                          unsigned long long* __restrict__ stamps, double* __restrict__ gws,
+                                          const int sol) {
     constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
     constexpr int NU = C::NU;   // (shadows the unicycle's mpcg::NU)
     constexpr int ZS = C::ZSL;  // slack variable (NB == 4)
@@ -698,7 +710,6 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
     __shared__ char lds_pad[MPCG_LDS_PAD];
     if (threadIdx.x == 1000) lds_pad[blockIdx.x % MPCG_LDS_PAD] = 0;
 #endif
-    const int sol = blockIdx.x;
     if (sol >= batch) return;
     // the lane exchanges assume one wavefront per workgroup (wave_sync): any other launch
     // shape reports an invalid exit code instead of racing
@@ -706,7 +717,11 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
         if (threadIdx.x == 0) io.exit_code[sol] = -1;
         return;
     }
-    const int lane = threadIdx.x;
+    // (laundered per solve: with the work queue this body is a loop, and nothing lane-dependent
+    // may be hoisted out of it to stay live across solves)
+    int lane_ = threadIdx.x;
+    if constexpr (C::QUEUE) __asm__ volatile("" : "+v"(lane_));
+    const int lane = lane_;
     const int k = lane / PARTS;          // my stage
     const int part = lane - k * PARTS;   // my part
     const bool stage_lane = (part == 0) && (k <= N);
@@ -2714,6 +2729,49 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
         }
     }
     STAMP_STORE(stamps, sol);
+}
+
+// The batched solve.  queue == NULL or an instance without C::QUEUE: workgroup b solves problem b
+// (a grid of `batch` workgroups).  Otherwise a grid of at most the resident workgroups (launch_instance: MPCG_QUEUE) takes the
+// problems from the head of a work queue, queue[0], one at a time until it runs past `batch`:
+// the hardware deals workgroups to the XCDs round robin and starts a new one only when a slot
+// frees, so with a grid of one workgroup per solve each XCD works through a fixed eighth of the
+// batch and every solve pays a workgroup launch; here a wave that finishes early takes the next
+// solve of the whole batch (the tail).  Every wave leaves the loop on its first
+// ticket >= batch; the last workgroup out (queue[1] counts them) zeroes both words for the next
+// launch on the same workspace, which the stream orders after this one.
+template <class C, bool FULL = false>
+__global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
+                                                    unsigned long long* __restrict__ stamps,
+                                                    double* __restrict__ gws, unsigned* __restrict__ queue) {
+    if constexpr (!C::QUEUE) {
+        (void)queue;
+        sqp_solve<C, FULL>(pr, batch, io, stamps, gws, blockIdx.x);
+    } else {
+        if (blockDim.x != 64) {
+            // the lane exchanges assume one wavefront per workgroup (wave_sync): any other launch
+            // shape reports an invalid exit code instead of racing
+            if (threadIdx.x == 0)
+                for (int sol = blockIdx.x; sol < batch; sol += gridDim.x) io.exit_code[sol] = -1;
+            return;
+        }
+        const bool q = queue != nullptr;
+        // (a ticket past INT_MAX -- a queue left non-zero by an aborted launch -- ends the loop too)
+        auto next = [&]() -> int {
+            unsigned t = 0;
+            if (threadIdx.x == 0) t = atomicAdd(&queue[0], 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            return t < (unsigned)batch ? (int)t : batch;
+        };
+        for (int sol = q ? next() : (int)blockIdx.x; sol < batch; sol = q ? next() : batch) {
+            sqp_solve<C, FULL>(pr, batch, io, stamps, gws, sol);
+            wave_sync();
+        }
+        if (q && threadIdx.x == 0 && atomicAdd(&queue[1], 1u) == gridDim.x - 1) {
+            atomicExch(&queue[0], 0u);
+            atomicExch(&queue[1], 0u);
+        }
+    }
 }
 
 }  // namespace mpcg
