@@ -19,7 +19,7 @@ SOURCES = {"mpcg_kernels.hip": [], "mpcg_prepare.hip": ["-ffp-contract=off"],
            # built-in kernel instances, one translation unit per family (compiled in parallel)
            "mpcg_inst_tmpc20.hip": [], "mpcg_inst_tmpc30.hip": [], "mpcg_inst_shmpc.hip": [],
            "mpcg_inst_bicycle.hip": []}
-HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_prepare.h", "mpcg_bicycle.h", "mpcg_instance.h"]
+HEADERS = ["mpcg_device.h", "mpcg_sqp.h", "mpcg_sqp_body.inc", "mpcg_prepare.h", "mpcg_bicycle.h", "mpcg_instance.h"]
 HOST_SOURCES = ["host/mpcg_yaml.cpp", "host/mpcg_solver.cpp"]
 HOST_HEADERS = ["mpc_planner_solver/mpcg_yaml.h", "mpc_planner_solver/mpcg_config.h", "mpc_planner_solver/state.h",
                 "mpc_planner_solver/mpcg_solver_interface.h", "mpc_planner_solver/solver_interface.h"]

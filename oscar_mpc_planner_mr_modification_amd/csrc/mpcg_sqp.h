@@ -657,2078 +657,7 @@ template <class C, bool FULL>
 __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io,
                                           unsigned long long* __restrict__ stamps, double* __restrict__ gws,
                                           const int sol) {
-    constexpr int N = C::N, PARTS = C::PARTS, NX = C::NX, NZ = C::NZ, NB = C::NB, NBT = C::NBT;
-    constexpr int NU = C::NU;   // (shadows the unicycle's mpcg::NU)
-    constexpr int ZS = C::ZSL;  // slack variable (NB == 4)
-    constexpr int X0 = C::IX, X1 = C::IY, X2 = C::IPSI;
-    constexpr bool LEAN = lds_lean<C>();
-    constexpr bool GFH = lds_gfh<C>();
-    // the predictor's barrier pass fused into the residual pass: its barrier terms come from the row
-    // state the residual pass has just computed, with the same operations, and one box-sum exchange,
-    // loop and fold fewer per interior-point iteration (wasted only on the iteration that exits).
-    // Measured (profiles/r03q_ab.jsonl, two alternating repetitions): C2 12.32 -> 11.97 ms, C1 10.61
-    // -> 10.43, C4 47.48 -> 45.38, C5 20.60 -> 19.46, JS 38.32 -> 37.17; C3 20.30 -> 19.81
-    // (profiles/r03s_ab.jsonl).  (MPCG_FUSE_BAR=0: A/B)
-#ifndef MPCG_FUSE_BAR
-#define MPCG_FUSE_BAR 1
-#endif
-    constexpr bool FUSE_BAR = MPCG_FUSE_BAR > 0;
-    // RES_SPLIT: the stage algebra of the residual and barrier passes (H dz, the stationarity rows,
-    // the Newton gradient, the dynamics rows) split over the parts of a stage -- part p owns the
-    // rows of its box variables p, p + PARTS, ... (and dynamics rows p, p + PARTS, ...), whose box
-    // sums it holds in registers -- instead of one stage lane doing all of them while the other
-    // parts wait.  Same operations per row.  Measured (profiles/r03r_ab.jsonl, two alternating
-    // repetitions): C2 11.99 -> 11.68 ms, C1 10.42 -> 10.15, C5 unchanged; on the two-part long
-    // horizons it moves the allocation into scratch (C4 45.29 -> 46.76, JD 40.45 -> 40.70, JS
-    // 37.25 -> 37.13), so three-part instances only; and not on the slack model, where it was neutral
-    // in time but moved the allocation into scratch (C5 52 -> 188 B/lane, 264 -> 782 MB of HBM traffic
-    // per launch, profiles/r03u_c5_pmc.json).  (MPCG_RES_SPLIT=0: off, 2: every instance)
-#ifndef MPCG_RES_SPLIT
-#define MPCG_RES_SPLIT 1
-#endif
-    constexpr bool RES_SPLIT = MPCG_RES_SPLIT > 0 && FUSE_BAR && !C::COMPACT && PARTS > 1 && 2 * NB <= NZ &&
-                               ((PARTS == 3 && NX == 5) || MPCG_RES_SPLIT > 1);
-    constexpr int DRS = (NX + PARTS - 1) / PARTS;  // dynamics rows per part
-    // MIRROR's eigenvector rows split over the parts of a stage (MPCG_MSPLIT=1, A/B only): bit-identical
-    // outputs (scripts/bitcmp.py on C2, C5, C4, JS: profiles/r03t_bitcmp.log) but slower everywhere --
-    // the stage matrix and row exchanges and the longer-lived state push the linearisation into
-    // scratch: C2 11.65 -> 12.46 ms, C1 10.16 -> 10.45, C4 45.41 -> 50.57, C5 19.47 -> 21.53, JS
-    // 37.24 -> 39.63, JD 40.56 -> 43.38 (profiles/r03t_ab.jsonl)
-#ifndef MPCG_MSPLIT
-#define MPCG_MSPLIT 0
-#endif
-    constexpr bool MSPLIT = MPCG_MSPLIT > 0 && C::MODEL == 0;
-    // the feedback's new dynamics multipliers split over the parts too (MPCG_PIN_SPLIT=1, A/B only:
-    // measured slower, C2 11.69 -> 11.78 ms, C1 10.16 -> 10.22, C5 unchanged; profiles/r03s_ab.jsonl)
-#ifndef MPCG_PIN_SPLIT
-#define MPCG_PIN_SPLIT 0
-#endif
-    constexpr bool PIN_SPLIT = MPCG_PIN_SPLIT > 0 && RES_SPLIT && !LEAN && C::CHAIN_SPLIT;
-    __shared__ LdsOf<C> S;
-#ifdef MPCG_LDS_PAD
-    // occupancy experiment only: pad the LDS footprint
-    __shared__ char lds_pad[MPCG_LDS_PAD];
-    if (threadIdx.x == 1000) lds_pad[blockIdx.x % MPCG_LDS_PAD] = 0;
-#endif
-    if (sol >= batch) return;
-    // the lane exchanges assume one wavefront per workgroup (wave_sync): any other launch
-    // shape reports an invalid exit code instead of racing
-    if (blockDim.x != 64) {
-        if (threadIdx.x == 0) io.exit_code[sol] = -1;
-        return;
-    }
-    // (laundered per solve: with the work queue this body is a loop, and nothing lane-dependent
-    // may be hoisted out of it to stay live across solves)
-    int lane_ = threadIdx.x;
-    if constexpr (C::QUEUE) __asm__ volatile("" : "+v"(lane_));
-    const int lane = lane_;
-    const int k = lane / PARTS;          // my stage
-    const int part = lane - k * PARTS;   // my part
-    const bool stage_lane = (part == 0) && (k <= N);
-    const int ks = k <= N ? k : N;       // clamped stage (always a valid LDS index)
-    const int kc = k < N ? k : N - 1;    // clamped stage < N
-    const int npar = pr.npar;
-    constexpr int LAMS = NX + C::NH;  // multiplier block per stage (include/mpcg.h, mpcg_io)
-#ifdef MPCG_DIAG_PARAMS_OF
-    // diagnostic build only (scripts/param_locality.py): solve sol reads the parameter block of
-    // solve sol % MPCG_DIAG_PARAMS_OF (a batch of identical copies: the cost of the parameter reads'
-    // misses)
-    const double* pbase = io.params + (size_t)(sol % MPCG_DIAG_PARAMS_OF) * N * npar;
-#else
-    const double* pbase = io.params + (size_t)sol * N * npar;
-#endif
-    const double* pk = pbase + (size_t)kc * npar;
-    (void)stamps;
-    // the stage blocks [B A] (Fb) and H (Hb): LDS, or this solve's global workspace (GFH)
-    double* const gF = GFH ? gws + (size_t)sol * gfh_doubles<C>() : nullptr;
-    double* const gH = GFH ? gF + (size_t)N * C::NFR * C::NFC : nullptr;
-    auto Fb = [&](int kq) -> double (*)[C::NFC] {
-        if constexpr (GFH) return (double (*)[C::NFC])(gF + (size_t)kq * C::NFR * C::NFC);
-        else return S.F[kq];
-    };
-    auto Hb = [&](int kq) -> double* {
-        if constexpr (GFH) return gH + (size_t)kq * C::NHP;
-        else return S.H[kq];
-    };
-    STAMP_DECL
-
-    // NLP multipliers carried over from the previous solve of this planner
-    // (zero for a fresh or reset acados capsule)
-    const double* lam_in = io.lam_in ? io.lam_in + (size_t)sol * N * LAMS : nullptr;
-    constexpr int BVS = C::BVS, HS = C::HS, HB = 2 * C::BVS;  // HB: first h slot
-    LaneRows<C> LR;
-    LR.k = k;
-    LR.part = part;
-    if constexpr (C::BOUNDS_SEL) {
-        LR.prb = &pr;
-    } else {
-#pragma unroll
-        for (int j = 0; j < BVS; ++j) {
-            const int v = LR.var(j);
-            double lo = 0.0, hi = 0.0;
-#pragma unroll
-            for (int i = 0; i < NZ; ++i)
-                if (v == i) { lo = i < NU ? pr.lbu[i] : pr.lbx[i - NU]; hi = i < NU ? pr.ubu[i] : pr.ubx[i - NU]; }
-            LR.lo[j] = lo;
-            LR.hi[j] = hi;
-        }
-    }
-    // gradient (x, y, psi) and gap of h row hh of this lane's stage
-    auto rowg = [&](int hh, double& a, double& b, double& c) {
-        if constexpr (C::LIN_PARAMS) {
-            if (hh < C::NL || hh >= C::NL + C::NE) {
-                const double* p = hh < C::NL ? pk + pr.i_lin0 + 3 * hh : pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
-                a = p[0];
-                b = p[1];
-                c = hh < C::NL ? 0.0 : p[0] * S.disc[k][2] + p[1] * S.disc[k][3];
-                return;
-            }
-            const int he = hh - C::NL;
-            a = S.Dg[k][he * C::DGC + 0];
-            b = S.Dg[k][he * C::DGC + 1];
-            c = a * S.disc[k][2] + b * S.disc[k][3];
-        } else {
-            a = S.Dg[k][hh * C::DGC + 0]; b = S.Dg[k][hh * C::DGC + 1]; c = S.Dg[k][hh * C::DGC + 2];
-        }
-    };
-    auto rowgap = [&](int hh) -> double {
-        if constexpr (C::LIN_PARAMS) {
-            const double x = S.z[k][X0], y = S.z[k][X1];
-            if (hh < C::NL) {
-                const double* p = pk + pr.i_lin0 + 3 * hh;
-                return 0.0 - (p[0] * x + p[1] * y - p[2]);
-            }
-            if (hh >= C::NL + C::NE) {
-                const double* p = pk + pr.i_scen0 + 3 * (hh - C::NL - C::NE);
-                const double sl = C::HAS_SLACK ? S.z[k][ZS] : 0.0;
-                return 0.0 - (p[0] * (x + S.disc[k][0]) + p[1] * (y + S.disc[k][1]) - (p[2] + sl));
-            }
-            return S.hd[k][hh - C::NL];
-        } else {
-            return S.hd[k][hh];
-        }
-    };
-    // [B A] and Hessian entries of stage kq (the compact C3 storage rebuilds the known ones)
-    // the s+ row's coefficients of a and v (uniform, bit-identical to erk_unicycle's)
-    double srow_a = 0.0, srow_v = 0.0;
-    if constexpr (C::FCONST) erk_srow(pr, srow_a, srow_v);
-    auto FatB = [&](const double (*Fk)[C::NFC], int m, int j) -> double {
-        if constexpr (C::FCONST) {
-            // rows psi+, v+, s+ (, slack+) are constants (z = [a w x y psi v s (slack)])
-            if (m == 2) return j == 1 ? pr.dt : (j == 4 ? 1.0 : 0.0);
-            if (m == 3) return j == 0 ? pr.dt : (j == 5 ? 1.0 : 0.0);
-            if (m == 4) return j == 0 ? srow_a : (j == 5 ? srow_v : (j == 6 ? 1.0 : 0.0));
-            if (m >= 5) return j == NU + m ? 1.0 : 0.0;
-            return Fk[m][j];
-        } else if constexpr (C::COMPACT) {
-            if (m == 3) return j == bike::ZV ? 1.0 : (j == bike::ZA ? pr.dt : 0.0);
-            if (m == 4) return j == bike::ZDELTA ? 1.0 : (j == bike::ZW ? pr.dt : 0.0);
-            if (j == ZS) return 0.0;
-            return Fk[m < 3 ? m : 3][j < ZS ? j : j - 1];
-        } else {
-            return Fk[m][j];
-        }
-    };
-    auto HatB = [&](const double* Hk, int i, int j) -> double {
-        if constexpr (C::COMPACT) {
-            if (i == ZS || j == ZS) return (i == j) ? Hk[C::NHP - 1] : 0.0;
-            return Hk[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
-        } else {
-            return Hk[sym(i, j)];
-        }
-    };
-    auto Fat = [&](int kq, int m, int j) -> double { return FatB(Fb(kq), m, j); };
-    auto Hat = [&](int kq, int i, int j) -> double { return HatB(Hb(kq), i, j); };
-    // dynamics residual b + F dz - dz+ of stage kq at the current QP iterate (same operation order
-    // as the residual phase, which stores it unless C::COMPACT)
-    auto rdyn_at = [&](int kq, int i) -> double {
-        double a = S.b[kq][i] - S.dz[kq + 1][NU + i];
-#pragma unroll
-        for (int j = 0; j < NZ; ++j) a += Fat(kq, i, j) * S.dz[kq][j];
-        return a;
-    };
-    Rows<C> R;
-#pragma unroll
-    for (int r = 0; r < HS; ++r) R.nlam[r] = (lam_in && LR.h_on(r)) ? lam_in[(size_t)k * LAMS + NX + LR.hrow(r)] : 0.0;
-
-    // ---- load warm start (loadWarmstart, acados_solver_interface.cpp:274-284)
-    const double* w = io.warm + (size_t)sol * (N + 1) * NZ;
-    for (int e = lane; e < (N + 1) * NZ; e += 64) (&S.z[0][0])[e] = w[e];
-    if (lane < NX) S.xinit[lane] = io.xinit[(size_t)sol * NX + lane];
-    for (int e = lane; e < N * NX; e += 64)
-        (&S.pi_nlp[0][0])[e] = lam_in ? lam_in[(size_t)(e / NX) * LAMS + e % NX] : 0.0;
-    for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
-    // the capsule's QP memory, if any: the previous QP's solution, whose row multipliers are
-    // also the NLP's (FIXED_STEP) -- read by the NLP residuals -- and, with the HPIPM warm
-    // start (qp_solver_warm_start 2), the initial point of the first QP; the later QPs
-    // start from their predecessor's solution
-    const bool qp_warm = FULL && pr.qp_warm_start == 2;
-    // solver_type SQP: one acados SQP call (acados_solver_interface.cpp:27-29), terminated by the
-    // NLP residuals (FULL only)
-    const bool sqp_mode = FULL && pr.nlp_solver == MPCG_NLP_SQP;
-    bool have_qp = false;
-    if (FULL && io.qp_in && !isnan(io.qp_in[(size_t)sol * C::QPM])) {
-        const double* q = io.qp_in + (size_t)sol * C::QPM;
-#pragma unroll
-        for (int sl = 0; sl < C::SLOTS; ++sl) {
-            R.t[sl] = q[(2 * sl) * 64 + lane];
-            R.l[sl] = q[(2 * sl + 1) * 64 + lane];
-        }
-        for (int e = lane; e < (N + 1) * NZ; e += 64) (&S.dz[0][0])[e] = q[C::QPM_ROWS + e];
-        for (int e = lane; e < N * NX; e += 64) (&S.piq[0][0])[e] = q[C::QPM_ROWS + (N + 1) * NZ + e];
-        have_qp = true;
-    }
-    wave_sync();
-    if (lane < NU) S.z[N][lane] = 0.0;
-    wave_sync();
-
-    // the interior point's divergence test and t / lambda floor, read once
-    const double mu_max = pr.qp_mu_max, tmin = pr.qp_t_min;
-    int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_total = 0, n_maxit = 0;
-    double res_eq = 0.0;
-    double nlp_stat = 0.0, nlp_ineq = 0.0, nlp_comp = 0.0;  // NLP residuals of the last linearisation
-    bool nlp_nonfinite = false;
-
-    for (int it = 0; sqp_mode || it < pr.sqp_iters; ++it) {
-        // parameter loads are re-issued where they are used rather than hoisted out of
-        // the SQP / QP loops into registers that stay live (and spill) across them
-        if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
-        // =============== preparation: linearise every stage ===============
-        STAMP_BEGIN();
-        {
-            double zk[NZ];
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) zk[i] = S.z[ks][i];
-            double hb6[6] = {0, 0, 0, 0, 0, 0};
-            if (k >= 1 && k < N) h_rows<C>(pr, pk, zk, LR, R.nlam, hb6, (double (*)[C::DGC])S.Dg[k], S.hd[k], S.disc[C::LIN_PARAMS ? k : 0]);
-            STAMP_LAP(10);
-            // fold the h-row Hessian terms of parts 1.. into part 0 (fixed order)
-            {
-                double acc[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) acc[i] = hb6[i];
-#pragma unroll
-                for (int p = 1; p < PARTS; ++p)
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) acc[i] += lane_down(hb6[i], p);
-#pragma unroll
-                for (int i = 0; i < 6; ++i) hb6[i] = acc[i];
-            }
-            double resl = 0.0;
-            // MSPLIT: the MIRROR sweeps run on all parts of a stage, each accumulating its rows of the
-            // eigenvectors (mirror_rows); the stage matrix goes out from part 0 and the other parts'
-            // rows come back through MX, a per-stage exchange area over the Riccati arrays P, Lc, Y
-            // and the box sums (all dead during the linearisation)
-            constexpr int MNA = NZ == 8 ? NZ - 1 : NZ;  // the slack model's decoupled slack diagonal aside
-            constexpr int MRV = (MNA + PARTS - 1) / PARTS;
-            constexpr int MXS = imax(MNA * (MNA + 1) / 2, (MNA - (MNA + PARTS - 1) / PARTS) * MNA) + 1;
-            double* const MX = &S.P[0][0];
-            static_assert(!MSPLIT || offsetof(LdsOf<C>, Dg) - offsetof(LdsOf<C>, P) >= sizeof(double) * N * MXS,
-                          "MIRROR exchange area (P, Lc, Y, bx)");
-            double H[NZ][NZ];
-            if (stage_lane && k < N) {
-                double g[NZ], xn[NX], pi[NX];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) pi[i] = S.pi_nlp[k][i];
-                if constexpr (C::MODEL == 1) {
-                    // the bicycle: the discrete map first (F and its Hessian straight to the stage's
-                    // LDS blocks, H[k] rewritten below), then the cost, so that the map's jets and the
-                    // 9x9 cost block are not live together
-                    double* const Hd = Hb(k);
-                    bike::discrete(pr, pk, zk, pi, xn, Fb(k), Hd);
-                    STAMP_LAP(12);
-                    bike::stage_cost(pr, pk, k, zk, g, H, true);
-                    STAMP_LAP(11);
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j)
-                            if (i != ZS && j != ZS) H[i][j] += Hd[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        const double bi = xn[i] - S.z[k + 1][NU + i];
-                        S.b[k][i] = bi;
-                        resl = fmax(resl, fabs(bi));
-                    }
-                } else {
-                    double F[NX][NZ];
-                    stage_cost<NX>(pr, pk, zk, g, H, true);
-                    STAMP_LAP(11);
-                    erk_unicycle<NX>(pr, zk, pi, xn, F, H);
-                    STAMP_LAP(12);
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        const double bi = xn[i] - S.z[k + 1][NU + i];
-                        S.b[k][i] = bi;
-                        resl = fmax(resl, fabs(bi));
-                        if (i < C::NFR) {
-#pragma unroll
-                            for (int j = 0; j < NZ; ++j) Fb(k)[i][j] = F[i][j];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) S.g[k][i] = g[i];
-                H[X0][X0] += hb6[0]; H[X0][X1] += hb6[1]; H[X1][X0] += hb6[1];
-                H[X0][X2] += hb6[2]; H[X2][X0] += hb6[2];
-                H[X1][X1] += hb6[3]; H[X1][X2] += hb6[4]; H[X2][X1] += hb6[4];
-                H[X2][X2] += hb6[5];
-                STAMP_LAP(13);
-                if constexpr (MSPLIT) {
-                    // mirror()'s symmetrisation, then the upper triangle (and the slack diagonal's
-                    // square, which enters the sweeps' convergence test) to the stage's exchange slot
-#pragma unroll
-                    for (int i = 0; i < MNA; ++i)
-#pragma unroll
-                        for (int j = i + 1; j < MNA; ++j) H[i][j] = 0.5 * (H[i][j] + H[j][i]);
-#pragma unroll
-                    for (int i = 0; i < MNA; ++i)
-#pragma unroll
-                        for (int j = i; j < MNA; ++j) MX[k * MXS + sym(j, i)] = H[i][j];
-                    MX[k * MXS + MXS - 1] = NZ == 8 ? H[NZ - 1][NZ - 1] * H[NZ - 1][NZ - 1] : 0.0;
-                } else if constexpr (C::MODEL == 0 && NZ == 8) {
-                    // the slack row/column of the slack model is exactly zero off the
-                    // diagonal (quadratic slack cost, linear in every h row, no dynamics
-                    // coupling): MIRROR of the 8x8 block = MIRROR of the leading 7x7 block
-                    // plus the mirrored slack diagonal, with the same sweep count
-                    const double hs = H[NZ - 1][NZ - 1];
-                    mirror<NZ, NZ - 1>(H, pr.reg_eps, hs * hs);
-                    H[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
-                } else if constexpr (C::MODEL == 1) {
-                    // the bicycle's slack input is decoupled the same way (quadratic cost, linear
-                    // in the decomp rows, no dynamics): with the slack moved last, MIRROR of the
-                    // leading 8x8 block (the 9x9 sweep's rotation order restricted to the other
-                    // variables) plus the mirrored slack diagonal
-                    double Hp[NZ][NZ];
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) {
-                            const int pi2 = i == NZ - 1 ? ZS : (i < ZS ? i : i + 1);
-                            const int pj2 = j == NZ - 1 ? ZS : (j < ZS ? j : j + 1);
-                            Hp[i][j] = H[pi2][pj2];
-                        }
-                    const double hs = Hp[NZ - 1][NZ - 1];
-                    mirror<NZ, NZ - 1>(Hp, pr.reg_eps, hs * hs);
-                    Hp[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) {
-                            const int pi2 = i == NZ - 1 ? ZS : (i < ZS ? i : i + 1);
-                            const int pj2 = j == NZ - 1 ? ZS : (j < ZS ? j : j + 1);
-                            H[pi2][pj2] = Hp[i][j];
-                        }
-                } else {
-                    mirror<NZ>(H, pr.reg_eps);
-                }
-                STAMP_LAP(14);
-                if constexpr (MSPLIT) {
-                } else if constexpr (C::COMPACT) {
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                        for (int j = 0; j <= i; ++j)
-                            if (i != ZS && j != ZS) Hb(k)[sym(i < ZS ? i : i - 1, j < ZS ? j : j - 1)] = H[i][j];
-                    Hb(k)[C::NHP - 1] = H[ZS][ZS];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                        for (int j = 0; j <= i; ++j) Hb(k)[sym(i, j)] = H[i][j];
-                }
-            } else if (stage_lane && k == N) {
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) S.g[N][i] = 0.0;
-#pragma unroll
-                for (int e = 0; e < C::NHP; ++e) Hb(N)[e] = 0.0;
-#pragma unroll
-                for (int i = NU; i < NZ; ++i) {
-                    if constexpr (C::COMPACT) Hb(N)[sym(i - 1, i - 1)] = pr.reg_eps;
-                    else Hb(N)[sym(i, i)] = pr.reg_eps;
-                }
-            }
-            if constexpr (MSPLIT) {
-                wave_sync();
-                if (k < N) {
-                    double dx2 = 0.0;
-                    if (part != 0) {
-#pragma unroll
-                        for (int i = 0; i < MNA; ++i)
-#pragma unroll
-                            for (int j = i; j < MNA; ++j) H[i][j] = MX[k * MXS + sym(j, i)];
-                    }
-                    dx2 = MX[k * MXS + MXS - 1];
-                    double Vr[MRV][MNA];
-                    mirror_rows<NZ, MNA, PARTS>(H, Vr, part, dx2);
-                    wave_sync();  // every part has read the stage matrix
-                    if (part != 0) {
-#pragma unroll
-                        for (int t = 0; t < MRV; ++t) {
-                            const int r = part + PARTS * t;
-                            if (r >= MNA) continue;
-                            const int sl = r - 1 - (r - 1) / PARTS;  // rank among the rows of parts 1..
-#pragma unroll
-                            for (int j = 0; j < MNA; ++j) MX[k * MXS + sl * MNA + j] = Vr[t][j];
-                        }
-                    }
-                    wave_sync();
-                    if (part == 0) {
-                        double V[MNA][MNA];
-#pragma unroll
-                        for (int r = 0; r < MNA; ++r) {
-                            if (r % PARTS == 0) {
-#pragma unroll
-                                for (int j = 0; j < MNA; ++j) V[r][j] = Vr[r / PARTS][j];
-                            } else {
-                                const int sl = r - 1 - (r - 1) / PARTS;
-#pragma unroll
-                                for (int j = 0; j < MNA; ++j) V[r][j] = MX[k * MXS + sl * MNA + j];
-                            }
-                        }
-                        mirror_rebuild<NZ, MNA>(H, V, pr.reg_eps);
-                        if constexpr (NZ == 8) {
-                            const double hs = H[NZ - 1][NZ - 1];
-                            H[NZ - 1][NZ - 1] = (hs >= -pr.reg_eps && hs <= pr.reg_eps) ? pr.reg_eps : fabs(hs);
-                        }
-#pragma unroll
-                        for (int i = 0; i < NZ; ++i)
-#pragma unroll
-                            for (int j = 0; j <= i; ++j) Hb(k)[sym(i, j)] = H[i][j];
-                    }
-                }
-            }
-            res_eq = wave_max(resl);
-            if (lane < NX) S.dz[0][NU + lane] = S.xinit[lane] - S.z[0][NU + lane];
-        }
-        // GFH: the stage lanes' global stores of the blocks complete before any lane reads them
-        if constexpr (GFH) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        wave_sync();
-        STAMP_END(0);
-
-        // =============== feedback: QP by Riccati interior point ===============
-        STAMP_BEGIN();
-        if (FULL && (io.stats || sqp_mode)) {
-            // NLP residuals at the linearisation point (acados ocp_nlp_res_compute) with the
-            // multipliers the NLP holds: pi_nlp and, per row, the previous QP's multiplier
-            // (FIXED_STEP: lam = lam_qp) or, before any QP, the carried h-row ones (box 0)
-            double rh[NB];
-#pragma unroll
-            for (int i = 0; i < NB; ++i) rh[i] = 0.0;
-            double vin = 0.0, vcp = 0.0, vst = 0.0;
-            // non-finite guard: 0 x every residual operand is NaN iff the operand is not finite (the
-            // fmax reductions below drop NaN, so a NaN iterate could otherwise pass the SQP test)
-            double chk = 0.0;
-#pragma unroll
-            for (int j = 0; j < BVS; ++j) {
-                double lb = 0.0;
-                if (LR.box_on(j)) {
-                    const double zv = S.z[k][LR.var(j)];
-                    const double gl = zv - LR.lo_at(j), gh = LR.hi_at(j) - zv;
-                    const double ll = have_qp ? R.l[2 * j] : 0.0, lh = have_qp ? R.l[2 * j + 1] : 0.0;
-                    chk += 0.0 * (zv + ll + lh);
-                    vin = fmax(vin, -gl);
-                    vin = fmax(vin, -gh);
-                    vcp = fmax(vcp, fabs(ll * gl));
-                    vcp = fmax(vcp, fabs(lh * gh));
-                    lb = lh - ll;
-                }
-                if (k <= N && LR.var(j) < NZ) S.bx[k][LR.var(j)] = lb;
-            }
-#pragma unroll
-            for (int r = 0; r < HS; ++r) {
-                if (!LR.h_on(r)) continue;
-                const int hh = LR.hrow(r);
-                double a, bq, c;
-                rowg(hh, a, bq, c);
-                const double gap = rowgap(hh);
-                const double lam = have_qp ? R.l[HB + r] : R.nlam[r];
-                rh[0] += a * lam; rh[1] += bq * lam; rh[2] += c * lam;
-                if constexpr (NB == 4) rh[3] += C::slack_coef(hh) * lam;
-                vin = fmax(vin, -gap);
-                vcp = fmax(vcp, fabs(lam * gap));
-                chk += 0.0 * (gap + lam);
-            }
-            double acc[NB];
-#pragma unroll
-            for (int i = 0; i < NB; ++i) acc[i] = rh[i];
-#pragma unroll
-            for (int p = 1; p < PARTS; ++p)
-#pragma unroll
-                for (int i = 0; i < NB; ++i) acc[i] += lane_down(rh[i], p);
-            wave_sync();  // the owner lanes' box sums S.bx
-            if (stage_lane) {
-                double r[NZ];
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) r[i] = S.g[k][i] + S.bx[k][i];
-#pragma unroll
-                for (int i = 0; i < NB; ++i) r[C::bvar(i)] += acc[i];
-                if (k < N) {
-#pragma unroll
-                    for (int m = 0; m < NX; ++m) {
-                        const double pm = S.pi_nlp[k][m];
-#pragma unroll
-                        for (int i = 0; i < NZ; ++i) r[i] += Fat(k, m, i) * pm;
-                    }
-                }
-                if (k > 0) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) r[NU + i] -= S.pi_nlp[k - 1][i];
-                }
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) {
-                    const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
-                    if (free_var) vst = fmax(vst, fabs(r[i]));
-                    chk += 0.0 * r[i];
-                }
-                if (k < N) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) chk += 0.0 * S.b[k][i];  // res_eq's operands
-                }
-            }
-            nlp_stat = wave_max(vst);
-            nlp_ineq = wave_max(vin);
-            nlp_comp = wave_max(vcp);
-            nlp_nonfinite = !(wave_sum(chk) == 0.0);
-            wave_sync();
-        }
-        if (sqp_mode) {
-            // a non-finite NLP residual ends the call with the NaN status (an iterate gone non-finite
-            // after an applied max-iter QP step would otherwise run every remaining iteration)
-            if (nlp_nonfinite) {
-                acados_status = AC_NAN;
-                break;
-            }
-            // acados SQP: converged at this linearisation point, or out of iterations (its
-            // residuals and res_eq are the final iterate's either way)
-            if (nlp_stat < pr.nlp_tol && res_eq < pr.nlp_tol && nlp_ineq < pr.nlp_tol && nlp_comp < pr.nlp_tol) {
-                acados_status = AC_SUCCESS;
-                break;
-            }
-            if (it >= pr.nlp_max_iter) {
-                acados_status = AC_MAXITER;
-                break;
-            }
-        }
-        // HPIPM warm start for every QP of an acados call after its first (SQP: it > 0), and for
-        // the first with warm_start_first_qp; SQP-RTI calls consist of one QP each
-        const bool warm_now = qp_warm && have_qp && ((sqp_mode && it > 0) || pr.qp_warm_first);
-        if (warm_now) {
-            // HPIPM warm_start 2 (d_ocp_qp_ipm init_var): the previous QP's solution is the
-            // initial point -- step and dynamics multipliers stay in LDS, the rows' slacks and
-            // multipliers in registers -- with slacks and multipliers clipped below at thr0
-            const double thr = pr.qp_ws_thr;
-#pragma unroll
-            for (int sl = 0; sl < C::SLOTS; ++sl) {
-                if (R.t[sl] < thr) R.t[sl] = thr;
-                if (R.l[sl] < thr) R.l[sl] = thr;
-                R.pr[sl] = 0.0;
-            }
-        } else {
-        // cold start: t = max(gap, thr0), l = mu0 / t
-        {
-            auto cold = [&](int s, double gap) {
-                const double t0 = gap > pr.qp_thr0 ? gap : pr.qp_thr0;
-                R.t[s] = t0;
-                R.l[s] = pr.qp_mu0 / t0;
-                R.pr[s] = 0.0;
-            };
-            // every slot is (re)written, inactive ones with placeholders that are never
-            // read: the row state is then dead between two QPs and the linearisation
-            // does not have to keep it in registers
-#pragma unroll
-            for (int j = 0; j < BVS; ++j) {
-                const bool on = LR.box_on(j);
-                const double zv = S.z[ks][on ? LR.var(j) : 0];
-                cold(2 * j, on ? zv - LR.lo_at(j) : 1.0);
-                cold(2 * j + 1, on ? LR.hi_at(j) - zv : 1.0);
-            }
-#pragma unroll
-            for (int r = 0; r < HS; ++r) {
-                const bool on = LR.h_on(r);
-                cold(HB + r, on ? rowgap(on ? LR.hrow(r) : 0) : 1.0);
-            }
-        }
-        if (stage_lane) {
-#pragma unroll
-            for (int i = 0; i < NZ; ++i)
-                if (!(k == 0 && i >= NU)) S.dz[k][i] = 0.0;
-            if (k < N) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) S.piq[k][i] = 0.0;
-            }
-        }
-        }
-        have_qp = true;
-        wave_sync();
-        STAMP_END(1);
-        int qstat = AC_MAXITER, qit = 0;
-        double pinr[LEAN ? NX : 1];  // LEAN: the new dynamics multipliers of the own stage
-        double Hdz[RES_SPLIT ? BVS : NZ];  // H_k dz_k of the current iterate: part 0 (RES_SPLIT: the lane's variables)
-        for (;; ++qit) {
-            if constexpr (C::RELOAD_PARAMS) asm volatile("" : "+v"(pk));
-            // ---- residuals
-            STAMP_BEGIN();
-            double rs = 0.0, re = 0.0, ri = 0.0, comp = 0.0;
-            {
-                double zk[NZ], dzk[NZ];
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) { dzk[i] = S.dz[ks][i]; zk[i] = S.z[ks][i]; }
-                double rh[NB], qh[NB], dbh[NBT], rbj[BVS], qbj[BVS];
-#pragma unroll
-                for (int i = 0; i < NB; ++i) rh[i] = qh[i] = 0.0;
-#pragma unroll
-                for (int i = 0; i < NBT; ++i) dbh[i] = 0.0;
-                // FUSE_BAR: the predictor's barrier terms (rc = l t, the same operations as the
-                // barrier pass) from the row state just computed
-                auto bar0 = [&](int s, double& coef, double& wgt) {
-                    const double l = R.l[s], t = R.t[s], itt = R.it(s);
-                    const double rc = l * t;
-                    coef = l + (l * R.rin[s] - rc) * itt;
-                    wgt = l * itt;
-                };
-                auto row_res = [&](int s, double ddot, double gap) {
-                    const double l = R.l[s], t = R.t[s];
-                    const double rin = ddot + t - gap;
-                    R.rin[s] = rin;
-                    R.set_it(s, frcp(t));
-                    ri = fmax(ri, fabs(rin));
-                    comp += l * t;
-                };
-#pragma unroll
-                for (int j = 0; j < BVS; ++j) {
-                    double& rb = rbj[j];
-                    double& qb = qbj[j];
-                    double dd = 0.0;
-                    rb = qb = 0.0;
-                    if (LR.box_on(j)) {
-                        const int v = LR.var(j);
-                        const double zv = S.z[k][v], dzv = S.dz[k][v];
-                        rb = R.l[2 * j + 1] - R.l[2 * j];
-                        row_res(2 * j, -dzv, zv - LR.lo_at(j));
-                        row_res(2 * j + 1, dzv, LR.hi_at(j) - zv);
-                        if constexpr (FUSE_BAR) {
-                            double c0, w0, c1, w1;
-                            bar0(2 * j, c0, w0);
-                            bar0(2 * j + 1, c1, w1);
-                            qb = c1 - c0;
-                            dd = w0 + w1;
-                        }
-                    } else {
-                        R.rin[2 * j] = R.rin[2 * j + 1] = 0.0;
-                        R.set_it(2 * j, 1.0);
-                        R.set_it(2 * j + 1, 1.0);
-                    }
-                    if (k <= N && LR.var(j) < NZ) {
-                        if constexpr (!RES_SPLIT) S.bx[k][LR.var(j)] = rb;
-                        if constexpr (FUSE_BAR) {
-                            if constexpr (!RES_SPLIT) S.q[k][LR.var(j)] = qb;  // dead since the last vector pass
-                            S.dH[k][LR.var(j)] = dd;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < HS; ++r) {
-                    if (!LR.h_on(r)) {
-                        R.rin[HB + r] = 0.0;
-                        R.set_it(HB + r, 1.0);
-                        continue;
-                    }
-                    const int hh = LR.hrow(r);
-                    double a, bq, c;
-                    rowg(hh, a, bq, c);
-                    const double l = R.l[HB + r];
-                    rh[0] += a * l; rh[1] += bq * l; rh[2] += c * l;
-                    double dd = a * dzk[X0] + bq * dzk[X1] + c * dzk[X2];
-                    if constexpr (NB == 4) {
-                        const double sc = C::slack_coef(hh);
-                        rh[3] += sc * l;
-                        dd += sc * dzk[ZS];
-                    }
-                    row_res(HB + r, dd, rowgap(hh));
-                    if constexpr (FUSE_BAR) {
-                        double coef, wgt;
-                        bar0(HB + r, coef, wgt);
-                        double dg[NB];
-                        dg[0] = a; dg[1] = bq; dg[2] = c;
-                        if constexpr (NB == 4) dg[3] = C::slack_coef(hh);
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) qh[i] += dg[i] * coef;
-#pragma unroll
-                        for (int cc = 0; cc < NB; ++cc)
-#pragma unroll
-                            for (int aa = cc; aa < NB; ++aa) dbh[cpk(NB, aa, cc)] += dg[aa] * wgt * dg[cc];
-                    }
-                }
-                double acc[NB], aq[NB], ab[NBT];
-#pragma unroll
-                for (int i = 0; i < NB; ++i) { acc[i] = rh[i]; aq[i] = qh[i]; }
-#pragma unroll
-                for (int i = 0; i < NBT; ++i) ab[i] = dbh[i];
-#pragma unroll
-                for (int p = 1; p < PARTS; ++p) {
-#pragma unroll
-                    for (int i = 0; i < NB; ++i) acc[i] += lane_down(rh[i], p);
-                    if constexpr (FUSE_BAR) {
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) aq[i] += lane_down(qh[i], p);
-#pragma unroll
-                        for (int i = 0; i < NBT; ++i) ab[i] += lane_down(dbh[i], p);
-                    }
-                }
-                if constexpr (RES_SPLIT) {
-                    // part 0's stage sums of the h rows to the owners of the block variables
-                    if (stage_lane) {
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) { S.bx[k][i] = acc[i]; S.bx[k][NB + i] = aq[i]; }
-#pragma unroll
-                        for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
-                    }
-                    wave_sync();
-                    if (k <= N) {
-                        double pq[NX];
-#pragma unroll
-                        for (int m = 0; m < NX; ++m) pq[m] = k < N ? S.piq[k][m] : 0.0;
-#pragma unroll
-                        for (int j = 0; j < BVS; ++j) {
-                            const int v = LR.var(j);
-                            if (v >= NZ) continue;
-                            double a = 0.0;
-#pragma unroll
-                            for (int jj = 0; jj < NZ; ++jj) a += Hat(k, v, jj) * dzk[jj];
-                            Hdz[j] = a;
-                            const int bi = C::blk(v);
-                            double rbox = rbj[j];
-                            if (bi >= 0) rbox += S.bx[k][bi];
-                            double rr = a + S.g[k][v] + rbox;
-                            {
-                                // the predictor's Newton gradient (barrier pass)
-                                double qv = a + S.g[k][v] + qbj[j];
-                                if (bi >= 0) qv += S.bx[k][NB + bi];
-                                S.q[k][v] = qv;
-                            }
-                            if (k < N) {
-#pragma unroll
-                                for (int m = 0; m < NX; ++m) rr += Fat(k, m, v) * pq[m];
-                            }
-                            if (k > 0 && v >= NU) rr -= S.piq[k - 1][v - NU];
-                            const bool free_var = (k == N) ? (v >= NU) : ((k == 0) ? (v < NU) : true);
-                            if (free_var) rs = fmax(rs, fabs(rr));
-                        }
-                        if (k < N) {
-#pragma unroll
-                            for (int jd = 0; jd < DRS; ++jd) {
-                                const int i = part + PARTS * jd;
-                                if (i >= NX) continue;
-                                double a = S.b[k][i] - S.dz[k + 1][NU + i];
-#pragma unroll
-                                for (int jj = 0; jj < NZ; ++jj) a += Fat(k, i, jj) * dzk[jj];
-                                if constexpr (!LEAN) S.rdyn[k][i] = a;
-                                re = fmax(re, fabs(a));
-                            }
-                        }
-                    }
-                } else {
-                wave_sync();  // the owner lanes' box sums S.bx
-                if (stage_lane) {
-                    double rbox[NZ];
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i) rbox[i] = S.bx[k][i];
-#pragma unroll
-                    for (int i = 0; i < NB; ++i) rbox[C::bvar(i)] += acc[i];
-                    double r[NZ];
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i) {
-                        double a = 0.0;
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) a += Hat(k, i, j) * dzk[j];
-                        if constexpr (!RES_SPLIT) Hdz[i] = a;
-                        r[i] = a + S.g[k][i] + rbox[i];
-                    }
-                    if constexpr (FUSE_BAR) {
-                        // the predictor's Newton gradient and h-row barrier block (barrier pass)
-#pragma unroll
-                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[RES_SPLIT ? 0 : i] + S.g[k][i] + S.q[k][i];
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) S.q[k][C::bvar(i)] += aq[i];
-#pragma unroll
-                        for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
-                    }
-                    if (k < N) {
-#pragma unroll
-                        for (int m = 0; m < NX; ++m) {
-                            const double pm = S.piq[k][m];
-#pragma unroll
-                            for (int i = 0; i < NZ; ++i) r[i] += Fat(k, m, i) * pm;
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = S.b[k][i] - S.dz[k + 1][NU + i];
-#pragma unroll
-                            for (int j = 0; j < NZ; ++j) a += Fat(k, i, j) * dzk[j];
-                            if constexpr (!LEAN) S.rdyn[k][i] = a;
-                            re = fmax(re, fabs(a));
-                        }
-                    }
-                    if (k > 0) {
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) r[NU + i] -= S.piq[k - 1][i];
-                    }
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i) {
-                        const bool free_var = (k == N) ? (i >= NU) : ((k == 0) ? (i < NU) : true);
-                        if (free_var) rs = fmax(rs, fabs(r[i]));
-                    }
-                }
-                }
-            }
-#ifdef MPCG_TRACE
-            rs = wave_max(rs);
-            re = wave_max(re);
-            ri = wave_max(ri);
-#else
-            // the exit tests compare all three residuals with the same bounds: one reduction of
-            // their lane maximum (fmax drops NaN exactly as the per-lane accumulation above does)
-            rs = wave_max(fmax(fmax(rs, re), ri));
-            re = ri = rs;
-#endif
-            comp = wave_sum(comp);
-            const double mu = comp / C::M_TOTAL;
-#ifdef MPCG_TRACE
-            // diagnostic build only (scripts/trace_solve.py): the oracle's ORC_DEBUG line of solve
-            // MPCG_TRACE (-1: every solve, prefixed with its index)
-            if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0)
-                printf("[%d]  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", sol, qit, rs, re, ri, mu);
-#endif
-            if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < mu_max)) { qstat = AC_NAN; break; }
-            if (rs < pr.qp_tol && re < pr.qp_tol && ri < pr.qp_tol && mu < pr.qp_tol) { qstat = AC_SUCCESS; break; }
-            if (qit >= pr.qp_iter_max) { qstat = AC_MAXITER; break; }
-            wave_sync();
-            STAMP_END(2);
-
-            double alpha = 1.0, sigma_mu = 0.0;
-            for (int phase = 0; phase < 2; ++phase) {
-                // ---- barrier terms + Newton gradient (FUSE_BAR: the predictor's came with the residuals)
-                STAMP_BEGIN();
-                if (!FUSE_BAR || phase == 1) {
-                    double qh[NB], dbh[NBT];
-#pragma unroll
-                    for (int i = 0; i < NB; ++i) qh[i] = 0.0;
-#pragma unroll
-                    for (int i = 0; i < NBT; ++i) dbh[i] = 0.0;
-                    // coef = l + (l rin - rc) / t, wgt = l / t of slot s
-                    auto bar = [&](int s, double& coef, double& wgt) {
-                        const double l = R.l[s], t = R.t[s], itt = R.it(s);
-                        const double rc = (phase == 0) ? l * t : l * t + R.pr[s] - sigma_mu;
-                        coef = l + (l * R.rin[s] - rc) * itt;
-                        wgt = l * itt;
-                    };
-                    double qbj[BVS];
-#pragma unroll
-                    for (int j = 0; j < BVS; ++j) {
-                        double qb = 0.0, dd = 0.0;
-                        if (LR.box_on(j)) {
-                            double c0, w0, c1, w1;
-                            bar(2 * j, c0, w0);
-                            bar(2 * j + 1, c1, w1);
-                            qb = c1 - c0;
-                            dd = w0 + w1;
-                        }
-                        qbj[j] = qb;
-                        if (k <= N && LR.var(j) < NZ) {
-                            if constexpr (!RES_SPLIT) S.bx[k][LR.var(j)] = qb;
-                            if (phase == 0) S.dH[k][LR.var(j)] = dd;
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < HS; ++r) {
-                        if (!LR.h_on(r)) continue;
-                        const int hh = LR.hrow(r);
-                        double coef, wgt;
-                        bar(HB + r, coef, wgt);
-                        double dg[NB];
-                        rowg(hh, dg[0], dg[1], dg[2]);
-                        if constexpr (NB == 4) dg[3] = C::slack_coef(hh);
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) qh[i] += dg[i] * coef;
-                        if (phase == 0) {
-#pragma unroll
-                            for (int c = 0; c < NB; ++c)
-#pragma unroll
-                                for (int a = c; a < NB; ++a) dbh[cpk(NB, a, c)] += dg[a] * wgt * dg[c];
-                        }
-                    }
-                    double aq[NB], ab[NBT];
-#pragma unroll
-                    for (int i = 0; i < NB; ++i) aq[i] = qh[i];
-#pragma unroll
-                    for (int i = 0; i < NBT; ++i) ab[i] = dbh[i];
-#pragma unroll
-                    for (int p = 1; p < PARTS; ++p) {
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) aq[i] += lane_down(qh[i], p);
-                        if (phase == 0) {
-#pragma unroll
-                            for (int i = 0; i < NBT; ++i) ab[i] += lane_down(dbh[i], p);
-                        }
-                    }
-                    if constexpr (RES_SPLIT) {
-                        // part 0's h-row sums to the owners of the block variables, then every
-                        // owner its variables' entries of the Newton gradient
-                        if (stage_lane) {
-#pragma unroll
-                            for (int i = 0; i < NB; ++i) S.bx[k][i] = aq[i];
-                        }
-                        wave_sync();
-                        if (k <= N) {
-#pragma unroll
-                            for (int j = 0; j < BVS; ++j) {
-                                const int v = LR.var(j);
-                                if (v >= NZ) continue;
-                                const int bi = C::blk(v);
-                                double qv = Hdz[j] + S.g[k][v] + qbj[j];
-                                if (bi >= 0) qv += S.bx[k][bi];
-                                S.q[k][v] = qv;
-                            }
-                        }
-                    } else {
-                    wave_sync();  // the owner lanes' box sums S.bx
-                    if (stage_lane) {
-#pragma unroll
-                        for (int i = 0; i < NZ; ++i) S.q[k][i] = Hdz[RES_SPLIT ? 0 : i] + S.g[k][i] + S.bx[k][i];
-#pragma unroll
-                        for (int i = 0; i < NB; ++i) S.q[k][C::bvar(i)] += aq[i];
-                        if (phase == 0) {
-#pragma unroll
-                            for (int i = 0; i < NBT; ++i) S.dH[k][NZ + i] = ab[i];
-                        }
-                    }
-                    }
-                    wave_sync();
-                }
-                STAMP_END(3);
-                // ---- Riccati factorisation (predictor only; the corrector reuses it)
-                STAMP_BEGIN();
-                if (phase == 0) {
-                    constexpr int NT = C::NTRI, NP = C::NPT, DZ = C::NDH - 1;
-                    constexpr bool FAC_FLAT = C::FAC_FLAT;
-                    // FAC_PAIR: two lanes per block entry (lanes 2e, 2e + 1 of entry e), each forming the
-                    // cost-to-go product P F[:, ej] on half of the rows (0-2 / 3-4) and its part of
-                    // F[:, ei]' (P F[:, ej]); a DPP add joins the halves.  18 fp64 FMAs per lane and step
-                    // instead of 30 (the nz 7 unicycle: 28 entries, 56 lanes)
-#ifndef MPCG_FAC_PAIR
-#define MPCG_FAC_PAIR 0
-#endif
-                    constexpr bool PAIR_EL = MPCG_FAC_PAIR && FAC_FLAT && NU == 2 && NX == 5 && !C::COMPACT &&
-                                             !C::FCONST && !GFH && 2 * NT <= 64;
-                    constexpr int RH = PAIR_EL ? 3 : NX;  // cost-to-go rows per lane
-                    const int el = PAIR_EL ? (lane >> 1) : lane;  // the lane's block entry
-                    const int half = PAIR_EL ? (lane & 1) : 0;
-                    // the lane's rows of P F (half 1: rows 3, 4 and a dummy row 4 with a zero weight)
-                    auto prow = [&](int t) -> int { return PAIR_EL ? (half == 0 ? t : (t < 2 ? 3 + t : 4)) : t; };
-                    auto prow_on = [&](int t) -> bool { return !PAIR_EL || half == 0 || t < 2; };
-                    // element lane -> (ei, ej), ei >= ej, of the nz x nz block
-                    int ei = 0;
-                    while ((ei + 1) * (ei + 2) / 2 <= el && ei < NZ - 1) ++ei;
-                    const int ej = el < NT ? el - ei * (ei + 1) / 2 : 0;
-                    // barrier entries of (ei, ej); DZ is the always-zero slot
-                    const int dhd = (ei == ej) ? ei : DZ;
-                    int dhb = DZ;
-                    {
-                        const int a = C::blk(ei), c = C::blk(ej);
-                        if (a >= 0 && c >= 0) dhb = NZ + (a >= c ? cpk(NB, a, c) : cpk(NB, c, a));
-                    }
-                    // P lanes: (pi_, pj_) of the nx x nx block
-                    int pi_ = 0;
-                    while ((pi_ + 1) * (pi_ + 2) / 2 <= lane && pi_ < NX - 1) ++pi_;
-                    const int pj_ = lane < NP ? lane - pi_ * (pi_ + 1) / 2 : 0;
-                    if (lane < NP) S.P[N][lane] = Hat(N, NU + pi_, NU + pj_) + dh_at<C>(S.dH[N], NU + pi_, NU + pj_);
-                    // failed pivots accumulate in a register and are voted once after the
-                    // recursion (a store under a branch inside the stage loop kept the
-                    // scheduler from hoisting the next LDS reads over it).  The register-starved
-                    // bicycle instance keeps the LDS flag: there the hoisted reads spill.
-                    bool fbad = false;
-                    if (!FAC_FLAT && lane == 0) S.flag = 0;
-                    wave_sync();
-                    // prefetch of stage N-1's block
-                    const int le = el < NT ? el : 0;
-                    double fi[NX], fj[NX], hv;
-#pragma unroll
-                    for (int m = 0; m < NX; ++m) fj[m] = Fat(N - 1, m, ej);
-#pragma unroll
-                    for (int t = 0; t < RH; ++t) fi[t] = prow_on(t) ? Fat(N - 1, prow(t), ei) : 0.0;
-                    // rows of [B A] that vary over the stages: with the constant rows (FCONST) only x+ and
-                    // y+; the others stay in fi / fj from the fill above (their per-stage re-evaluation
-                    // on the lane's runtime column compiled to branches inside the recursion)
-                    constexpr int NFV = C::FCONST ? C::NFR : NX;
-                    // (the compact bicycle storage: its v+ and delta+ rows are the known constants)
-                    auto varies = [](int m) { return !C::COMPACT || (m != 3 && m != 4); };
-                    // packed Hessian entry of the element lane (the compact storage: slack row / column 0
-                    // but the diagonal)
-                    auto Hel = [&](int kq) -> double {
-                        if constexpr (C::COMPACT) return Hat(kq, ei, ej);
-                        else return Hb(kq)[le];
-                    };
-                    // GFH: stage kn's blocks come from the staging copy (written this step from the
-                    // coalesced loads issued one step earlier)
-                    auto HelS = [&]() -> double {
-                        if constexpr (C::COMPACT) return HatB(S.Hst, ei, ej);
-                        else return S.Hst[le];
-                    };
-                    // measured: C4 53.40 -> 52.82 ms with the staging copy, C3 21.01 -> 21.67 (its
-                    // compact blocks are rebuilt entry by entry and the copy adds live state): C4 only
-#ifdef MPCG_NO_STAGE
-                    constexpr bool STG = false;  // A/B: the Riccati step reads the global blocks directly
-#else
-                    constexpr bool STG = GFH && !C::COMPACT;
-#endif
-                    constexpr int NFB = C::NFR * C::NFC;
-                    static_assert(!GFH || (NFB <= 64 && C::NHP <= 64), "one staged entry per lane");
-                    double gsf = 0.0, gsh = 0.0;  // the staged entries of the next block in flight
-                    auto stage_load = [&](int kq) {
-                        if constexpr (STG) {
-                            gsf = lane < NFB ? gF[(size_t)kq * NFB + lane] : 0.0;
-                            gsh = lane < C::NHP ? gH[(size_t)kq * C::NHP + lane] : 0.0;
-                        }
-                    };
-                    if (N >= 2) stage_load(N - 2);
-                    hv = Hel(N - 1) + S.dH[N - 1][dhd] + S.dH[N - 1][dhb];
-#pragma unroll
-                    for (int kk = N - 1; kk >= 0; --kk) {
-                        double Pm[NP];
-                        if constexpr (PAIR_EL) {
-                            // the lane's rows of the cost-to-go (two distinct addresses per read)
-#pragma unroll
-                            for (int t = 0; t < RH; ++t)
-#pragma unroll
-                                for (int l = 0; l < NX; ++l) Pm[t * NX + l] = S.P[kk + 1][sym(prow(t), l)];
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < NP; ++e) Pm[e] = S.P[kk + 1][e];
-                        }
-                        // prefetch of the next (lower) stage's block; it lands while this one is
-                        // reduced.  FAC_FLAT: every lane runs one branch-free block, the five row
-                        // products advance together, and the prefetch is issued after the pivot
-                        // block's reads (off the recursion's critical path, and not in front of
-                        // the LDS traffic the next step waits for)
-                        const int kn = kk > 0 ? kk - 1 : 0;
-                        if constexpr (STG) {
-                            // stage kn's blocks into the staging copy, then the loads of kn - 1
-                            if (lane < NFB) (&S.Fst[0][0])[lane] = gsf;
-                            if (lane < C::NHP) S.Hst[lane] = gsh;
-                            wave_sync();
-                            if (kk >= 2) stage_load(kk - 2);
-                        }
-                        double fi2[NX], fj2[NX], hv2;
-                        auto prefetch = [&]() {
-                            if constexpr (STG) {
-#pragma unroll
-                                for (int m = 0; m < NFV; ++m)
-                                    if (varies(m)) { fi2[m] = FatB(S.Fst, m, ei); fj2[m] = FatB(S.Fst, m, ej); }
-                                hv2 = HelS() + S.dH[kn][dhd] + S.dH[kn][dhb];
-                            } else if constexpr (PAIR_EL) {
-#pragma unroll
-                                for (int m = 0; m < NX; ++m) fj2[m] = Fat(kn, m, ej);
-#pragma unroll
-                                for (int t = 0; t < RH; ++t) fi2[t] = prow_on(t) ? Fat(kn, prow(t), ei) : 0.0;
-                                hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
-                            } else {
-#pragma unroll
-                                for (int m = 0; m < NFV; ++m)
-                                    if (varies(m)) { fi2[m] = Fat(kn, m, ei); fj2[m] = Fat(kn, m, ej); }
-                                hv2 = Hel(kn) + S.dH[kn][dhd] + S.dH[kn][dhb];
-                            }
-                        };
-                        if constexpr (!FAC_FLAT) prefetch();
-                        double v = hv;
-                        if constexpr (PAIR_EL) {
-                            // the lane's rows t of P F[:, ej], then its part of F[:, ei]' (P F[:, ej]) (half 1
-                            // starts from 0), the halves joined on the even lane (DPP row_shl:1)
-                            double tm[RH];
-#pragma unroll
-                            for (int t = 0; t < RH; ++t) tm[t] = 0.0;
-#pragma unroll
-                            for (int l = 0; l < NX; ++l)
-#pragma unroll
-                                for (int t = 0; t < RH; ++t) tm[t] += Pm[t * NX + l] * fj[l];
-                            v = half == 0 ? hv : 0.0;
-#pragma unroll
-                            for (int t = 0; t < RH; ++t) v += fi[t] * tm[t];
-                            v += dpp_d<0x101>(v);
-                            S.Msc[(el < NT && half == 0) ? el : 64 + lane] = v;
-                        } else if constexpr (FAC_FLAT) {
-                            double tm[NX];
-#pragma unroll
-                            for (int m = 0; m < NX; ++m) tm[m] = 0.0;
-#pragma unroll
-                            for (int l = 0; l < NX; ++l)
-#pragma unroll
-                                for (int m = 0; m < NX; ++m) tm[m] += Pm[sym(m, l)] * fj[l];
-#pragma unroll
-                            for (int m = 0; m < NX; ++m) v += fi[m] * tm[m];
-                            S.Msc[lane < NT ? lane : 64 + lane] = v;
-                        } else {
-#pragma unroll
-                            for (int m = 0; m < NX; ++m) {
-                                double tm = 0.0;
-#pragma unroll
-                                for (int l = 0; l < NX; ++l) tm += Pm[sym(m, l)] * fj[l];
-                                v += fi[m] * tm;
-                            }
-                            if (lane < NT) S.Msc[lane] = v;
-                        }
-                        STAMP_LAP(16);
-                        wave_sync();
-                        STAMP_LAP(17);
-                        if constexpr (NU == 2) {
-                          if (FAC_FLAT || lane < NP) {
-                            // the pivot block (element lanes 0, 1, 2) straight from their registers:
-                            // the recursion's critical path skips one LDS round trip
-                            constexpr int LS_ = PAIR_EL ? 2 : 1;  // lane stride of the block entries
-                            const double m00 = FAC_FLAT ? readlane_d(v, 0) : S.Msc[0];
-                            const double m10 = FAC_FLAT ? readlane_d(v, LS_) : S.Msc[1];
-                            const double m11 = FAC_FLAT ? readlane_d(v, 2 * LS_) : S.Msc[2];
-                            const double mi0 = S.Msc[sym(NU + pi_, 0)], mi1 = S.Msc[sym(NU + pi_, 1)];
-                            const double mj0 = S.Msc[sym(NU + pj_, 0)], mj1 = S.Msc[sym(NU + pj_, 1)];
-                            const double mij = S.Msc[sym(NU + pi_, NU + pj_)];
-                            if constexpr (FAC_FLAT) {
-                                __builtin_amdgcn_sched_barrier(0);
-                                prefetch();
-                                __builtin_amdgcn_sched_barrier(0);
-                            }
-                            // 2x2 Cholesky through reciprocal square roots
-                            // 1/l11 = sqrt(m00 / det) = l00 / sqrt(det): both reciprocal square
-                            // roots start from the block entries and run side by side
-                            const double il00 = frsq(m00);
-                            const double det = fma(m00, m11, -(m10 * m10));
-                            const double ild = frsq(det);
-                            const double l00 = m00 * il00;
-                            const double l10 = m10 * il00;
-                            const double il11 = l00 * ild;
-                            fbad = fbad | !(m00 > 0.0) | !(det > 0.0);
-                            const double y0i = mi0 * il00;
-                            const double y1i = (mi1 - l10 * y0i) * il11;
-                            const double y0j = mj0 * il00;
-                            const double y1j = (mj1 - l10 * y0j) * il11;
-                            *(lane < NP ? &S.P[kk][lane] : &S.Msc[64 + lane]) = mij - y0i * y0j - y1i * y1j;
-                            if (pj_ == 0 && lane < NP) { S.Y[kk][0][pi_] = y0i; S.Y[kk][1][pi_] = y1i; }
-                            if (lane == 0) { S.Lc[kk][0] = l00; S.Lc[kk][1] = l10; S.Lc[kk][2] = il00; S.Lc[kk][3] = il11; }
-                          }
-                        } else if (FAC_FLAT || lane < NP) {
-                            // Cholesky of Muu through reciprocal square roots
-                            double Lm[NU][NU], il[NU];
-                            bool bad = false;
-                            double Mu[C::NTRI > 0 ? NU * (NU + 1) / 2 : 1], Mi[NU], Mj[NU], mij = 0.0;
-                            if constexpr (FAC_FLAT) {
-#pragma unroll
-                                for (int e = 0; e < NU * (NU + 1) / 2; ++e) Mu[e] = S.Msc[e];
-#pragma unroll
-                                for (int u = 0; u < NU; ++u) { Mi[u] = S.Msc[sym(NU + pi_, u)]; Mj[u] = S.Msc[sym(NU + pj_, u)]; }
-                                mij = S.Msc[sym(NU + pi_, NU + pj_)];
-                                __builtin_amdgcn_sched_barrier(0);
-                                prefetch();
-                                __builtin_amdgcn_sched_barrier(0);
-                            }
-                            auto msc = [&](int i, int j) -> double {  // entry of the pivot block
-                                if constexpr (FAC_FLAT) return Mu[sym(i, j)];
-                                else return S.Msc[sym(i, j)];
-                            };
-#pragma unroll
-                            for (int j = 0; j < NU; ++j) {
-                                double d = msc(j, j);
-#pragma unroll
-                                for (int m = 0; m < j; ++m) d -= Lm[j][m] * Lm[j][m];
-                                il[j] = frsq(d);
-                                Lm[j][j] = d * il[j];
-                                bad = bad || !(d > 0.0);
-#pragma unroll
-                                for (int i = j + 1; i < NU; ++i) {
-                                    double acc = msc(i, j);
-#pragma unroll
-                                    for (int m = 0; m < j; ++m) acc -= Lm[i][m] * Lm[j][m];
-                                    Lm[i][j] = acc * il[j];
-                                }
-                            }
-                            if constexpr (FAC_FLAT) {
-                                fbad = fbad | bad;
-                            } else {
-                                if (bad) S.flag = 1;
-                            }
-                            double yi[NU], yj[NU];
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) {
-                                double ai = FAC_FLAT ? Mi[u] : S.Msc[sym(NU + pi_, u)];
-                                double aj = FAC_FLAT ? Mj[u] : S.Msc[sym(NU + pj_, u)];
-#pragma unroll
-                                for (int m = 0; m < u; ++m) { ai -= Lm[u][m] * yi[m]; aj -= Lm[u][m] * yj[m]; }
-                                yi[u] = ai * il[u];
-                                yj[u] = aj * il[u];
-                            }
-                            double pv = FAC_FLAT ? mij : S.Msc[sym(NU + pi_, NU + pj_)];
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) pv -= yi[u] * yj[u];
-                            *(lane < NP ? &S.P[kk][lane] : &S.Msc[64 + lane]) = pv;
-                            if (pj_ == 0 && lane < NP) {
-#pragma unroll
-                                for (int u = 0; u < NU; ++u) S.Y[kk][u][pi_] = yi[u];
-                            }
-                            if (lane == 0) {
-#pragma unroll
-                                for (int i = 1; i < NU; ++i)
-#pragma unroll
-                                    for (int j = 0; j < i; ++j) S.Lc[kk][C::lo_idx(i, j)] = Lm[i][j];
-#pragma unroll
-                                for (int u = 0; u < NU; ++u) S.Lc[kk][C::NLO + u] = il[u];
-                            }
-                        }
-#pragma unroll
-                        for (int m = 0; m < NFV; ++m)
-                            if (varies(m)) { fi[m] = fi2[m]; fj[m] = fj2[m]; }
-                        hv = hv2;
-                        STAMP_LAP(18);
-                        wave_sync();
-                        STAMP_LAP(19);
-                    }
-                    if (FAC_FLAT ? __any(fbad) : S.flag != 0) {
-#ifdef MPCG_TRACE
-                        if ((MPCG_TRACE < 0 || sol == MPCG_TRACE) && lane == 0) printf("[%d]  pivot failed\n", sol);
-#endif
-                        qstat = AC_NAN;
-                        break;
-                    }
-                }
-                STAMP_END(4);
-                // ---- vector + forward passes: affine 5-vector recursions in SGPRs
-                STAMP_BEGIN();
-                if constexpr (C::CHAIN_SPLIT) {
-                    // Every part of stage k owns the rows {part + PARTS s} of the stage's
-                    // backward map p_k = h_k + G_k p_{k+1} and the same columns of the forward
-                    // map dx_{k+1} = G_k' dx_k + e_k: a chain step is RS short dot products per
-                    // lane instead of one whole 5x5 product, and the owning parts' rows meet
-                    // in SGPRs through v_readlane.  Same operation order per row as the
-                    // single-owner chain (bit-identical).
-                    constexpr int RS = (NX + PARTS - 1) / PARTS;
-                    const int kv = k < N ? k : 0;
-                    const bool own = stage_lane && k < N;
-                    double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
-                    if constexpr (NU == 2) {
-                        Lo[0] = S.Lc[kv][1]; il[0] = S.Lc[kv][2]; il[1] = S.Lc[kv][3];
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kv][i];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) il[u] = S.Lc[kv][C::NLO + u];
-                    }
-                    // dynamics residual of stage kv (LEAN recomputes it)
-                    auto rdyn_v = [&](int i) -> double {
-                        if constexpr (LEAN) return rdyn_at(kv, i);
-                        else return S.rdyn[kv][i];
-                    };
-                    int rs[RS];
-                    bool rv[RS];
-#pragma unroll
-                    for (int t = 0; t < RS; ++t) {
-                        rv[t] = part + PARTS * t < NX;
-                        rs[t] = rv[t] ? part + PARTS * t : NX - 1;
-                    }
-                    double Wu[NU][NX], y0[NU], c[NX];
-                    {
-                        double rr[NX];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) rr[i] = rdyn_v(i);
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = 0.0;
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += S.P[kv + 1][sym(i, j)] * rr[j];
-                            c[i] = a;
-                        }
-                        double m0u[NU];
-#pragma unroll
-                        for (int i = 0; i < NU; ++i) {
-                            double a = S.q[kv][i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += Fat(kv, j, i) * c[j];
-                            m0u[i] = a;
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            double acc = m0u[u];
-#pragma unroll
-                            for (int m = 0; m < u; ++m) acc -= Lo[C::lo_idx(u, m)] * y0[m];
-                            y0[u] = acc * il[u];
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i)
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) {
-                                double w = Fat(kv, i, u);
-#pragma unroll
-                                for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wu[m][i];
-                                Wu[u][i] = w * il[u];
-                            }
-                    }
-                    // my rows of the backward map (h_r, G[r][.]) and columns of the forward one
-                    double hr[RS], Gr[RS][NX], Gc[RS][NX];
-#pragma unroll
-                    for (int t = 0; t < RS; ++t) {
-                        const int r = rs[t];
-                        double a = S.q[kv][NU + r];
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) a += Fat(kv, j, NU + r) * c[j];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) a -= S.Y[kv][u][r] * y0[u];
-                        hr[t] = a;
-                        double Yr[NU], Wr[NU];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) Yr[u] = S.Y[kv][u][r];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            double w = Fat(kv, r, u);
-#pragma unroll
-                            for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wr[m];
-                            Wr[u] = w * il[u];
-                        }
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) {
-                            double acc = Fat(kv, j, NU + r);
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) acc -= Yr[u] * Wu[u][j];
-                            Gr[t][j] = acc;
-                            double acc2 = Fat(kv, r, NU + j);
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) acc2 -= S.Y[kv][u][j] * Wr[u];
-                            Gc[t][j] = acc2;
-                        }
-                    }
-                    STAMP_LAP(6);
-                    double* const pch = &S.bx[0][0];
-                    static_assert((N + 1) * NZ >= N * NX, "chain storage");
-                    // Two-stage composed maps (PAIR): p_k = (h_k + G_k h_{k+1}) + G_k G_{k+1} p_{k+2}
-                    // on the stages k = N-2, N-4, ... (the chain), then p_k = h_k + G_k p_{k+1} on the
-                    // others, all at once; the forward map likewise (dx_{o+1} = Phi_o Phi_{o-1} dx_{o-1}
-                    // + Phi_o e_{o-1} + e_o on odd o, then the even stages).  Half the sequential
-                    // steps; each composition needs the partner stage's whole map, exchanged
-                    // through the barrier-term rows and the pivot scratch, both dead from the
-                    // Riccati step to the next barrier pass (which rewrites every barrier entry
-                    // but the always-zero slot, restored after the forward pass).
-                    constexpr bool PAIR = C::PAIR_CHAINS;
-                    constexpr int NSLOT = (N + 1) / 2;  // slots k >> 1 of the publishing stages k <= N - 1
-                    double* const XG = &S.dH[0][0];
-                    double* const Xh = &S.Msc[0];
-                    static_assert(!PAIR || (NSLOT * NX * NX <= (N + 1) * C::NDH && NSLOT * NX <= 128),
-                                  "pair exchange storage");
-                    // the stage's rows of (M, v) to its exchange slot / composed with the partner's slot
-                    auto publish = [&](int sl, const double (&M)[RS][NX], const double (&v)[RS]) {
-#pragma unroll
-                        for (int t = 0; t < RS; ++t) {
-                            if (!rv[t]) continue;
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) XG[(sl * NX + rs[t]) * NX + j] = M[t][j];
-                            Xh[sl * NX + rs[t]] = v[t];
-                        }
-                    };
-                    auto compose = [&](int sl, double (&M)[RS][NX], double (&v)[RS]) {
-                        double M2[RS][NX], v2[RS];
-#pragma unroll
-                        for (int t = 0; t < RS; ++t) {
-                            v2[t] = v[t];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) M2[t][j] = 0.0;
-                        }
-#pragma unroll
-                        for (int m = 0; m < NX; ++m) {
-                            const double hm = Xh[sl * NX + m];
-                            double xr[NX];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) xr[j] = XG[(sl * NX + m) * NX + j];
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                v2[t] += M[t][m] * hm;
-#pragma unroll
-                                for (int j = 0; j < NX; ++j) M2[t][j] += M[t][m] * xr[j];
-                            }
-                        }
-#pragma unroll
-                        for (int t = 0; t < RS; ++t) {
-                            v[t] = v2[t];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) M[t][j] = M2[t][j];
-                        }
-                    };
-                    // backward: the stages k = N-1, N-3, ... publish, k = N-2, N-4, ... compose
-                    const bool bfix = k >= 1 && k <= N - 1 && ((N - 1 - k) & 1) == 0;
-                    if constexpr (PAIR) {
-                        if (bfix) publish(k >> 1, Gr, hr);
-                        wave_sync();
-                        if (k >= 1 && k <= N - 2 && ((N - k) & 1) == 0) compose((k + 1) >> 1, Gr, hr);
-                    }
-                    double pu[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) pu[i] = S.q[N][NU + i];
-                    #pragma unroll
-                    for (int kk = PAIR ? N - 2 : N - 1; kk >= 1; kk -= PAIR ? 2 : 1) {  // p_0 is not needed
-                        double pn[RS];
-#pragma unroll
-                        for (int t = 0; t < RS; ++t) {
-                            pn[t] = chain_dot<NX>(hr[t], Gr[t], pu);
-                        }
-                        if constexpr (C::REC_FLAT) {
-                            // branch-free record: lanes that do not own the step write to the
-                            // dead pivot scratch (the stores then sink below the broadcast)
-#ifndef MPCG_REC_SELECT
-                            // owner lanes of step kk: the literal mask of stage kk's parts; both
-                            // candidate addresses are lane constants offset by the step's stride
-                            const unsigned long long OWN = ((1ull << PARTS) - 1) << (kk * PARTS);
-                            // dummies in the QP step rows (dead until the forward chain writes them)
-                            static_assert((N - 1) * NX + 8 <= (N + 1) * NZ, "record dummies inside the QP step rows");
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                const unsigned off = lds_addr(&S.ddz[0][lane & 7]);
-                                const unsigned on = rv[t] ? lds_addr(&pch[rs[t]]) : off;
-                                lds_store(sel_lanes(OWN, off, on) + kk * NX * 8, pn[t]);
-                            }
-#else
-#pragma unroll
-                            for (int t = 0; t < RS; ++t)
-                                *((k == kk && rv[t]) ? &pch[kk * NX + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = pn[t];
-#endif
-                        } else if (k == kk) {
-#pragma unroll
-                            for (int t = 0; t < RS; ++t)
-                                if (rv[t]) pch[kk * NX + rs[t]] = pn[t];
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) pu[i] = readlane_d(pn[i / PARTS], kk * PARTS + i % PARTS);
-                    }
-                    wave_sync();
-                    if constexpr (PAIR) {
-                        // the stages between the chain's: one map applied to the recorded p_{k+1}
-                        if (bfix) {
-                            const double* src = (k + 1 < N) ? pch + (k + 1) * NX : &S.q[N][NU];
-                            double pnx[NX];
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) pnx[i] = src[i];
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                double a = hr[t];
-#pragma unroll
-                                for (int j = 0; j < NX; ++j) a += Gr[t][j] * pnx[j];
-                                if (rv[t]) pch[k * NX + rs[t]] = a;
-                            }
-                        }
-                        wave_sync();
-                    }
-                    double pmine[NX];
-                    {
-                        const double* src = (kv + 1 < N) ? pch + (kv + 1) * NX : &S.q[N][NU];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) pmine[i] = src[i];
-                    }
-                    STAMP_LAP(15);
-                    // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
-                    double kf[NU];
-                    {
-                        double yy[NU];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            double acc = y0[u];
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) acc += Wu[u][i] * pmine[i];
-                            yy[u] = acc;
-                        }
-#pragma unroll
-                        for (int u = NU - 1; u >= 0; --u) {
-                            double acc = -yy[u];
-#pragma unroll
-                            for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * kf[m];
-                            kf[u] = acc * il[u];
-                        }
-                    }
-                    double ec[RS];
-#pragma unroll
-                    for (int t = 0; t < RS; ++t) {
-                        double acc = rdyn_v(rs[t]);
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) acc += Fat(kv, rs[t], u) * kf[u];
-                        ec[t] = acc;
-                    }
-                    // forward: the even stages publish (Phi_k, e_k), the odd stages compose
-                    const bool ffix = k <= N - 1 && (k & 1) == 0;
-                    if constexpr (PAIR) {
-                        if (ffix) publish(k >> 1, Gc, ec);
-                        wave_sync();
-                        if (k >= 1 && k <= N - 1 && (k & 1)) compose(k >> 1, Gc, ec);
-                    }
-                    // dx_{kk+1} goes straight to its place in the QP step, ddz[kk + 1]
-                    double dxu[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) dxu[i] = 0.0;
-                    #pragma unroll
-                    for (int kk = PAIR ? 1 : 0; kk < N; kk += PAIR ? 2 : 1) {
-                        double dn[RS];
-#pragma unroll
-                        for (int t = 0; t < RS; ++t) {
-                            dn[t] = chain_dot<NX>(ec[t], Gc[t], dxu);
-                        }
-                        if constexpr (C::REC_FLAT) {
-#ifndef MPCG_REC_SELECT
-                            // dummies in the box-sum rows (the backward chain's values are read)
-                            const unsigned long long OWN = ((1ull << PARTS) - 1) << (kk * PARTS);
-                            static_assert((N - 1) * NZ + 8 <= (N + 1) * NZ, "record dummies inside the box-sum rows");
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                const unsigned off = lds_addr(&S.bx[0][lane & 7]);
-                                const unsigned on = rv[t] ? lds_addr(&S.ddz[1][NU + rs[t]]) : off;
-                                lds_store(sel_lanes(OWN, off, on) + kk * NZ * 8, dn[t]);
-                            }
-#else
-#pragma unroll
-                            for (int t = 0; t < RS; ++t)
-                                *((k == kk && rv[t]) ? &S.ddz[kk + 1][NU + rs[t]] : &S.Msc[64 * (t & 1) + lane]) = dn[t];
-#endif
-                        } else if (k == kk) {
-#pragma unroll
-                            for (int t = 0; t < RS; ++t)
-                                if (rv[t]) S.ddz[kk + 1][NU + rs[t]] = dn[t];
-                        }
-                        if (kk + (PAIR ? 2 : 1) < N) {
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) dxu[i] = readlane_d(dn[i / PARTS], kk * PARTS + i % PARTS);
-                        }
-                    }
-                    wave_sync();
-                    if constexpr (PAIR) {
-                        // the even stages: one map applied to the recorded dx_k
-                        if (ffix) {
-                            double dxs[NX];
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) dxs[i] = k >= 1 ? S.ddz[k][NU + i] : 0.0;
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                double a = ec[t];
-#pragma unroll
-                                for (int j = 0; j < NX; ++j) a += Gc[t][j] * dxs[j];
-                                if (rv[t]) S.ddz[k + 1][NU + rs[t]] = a;
-                            }
-                        }
-                        // the barrier rows' always-zero slot, overwritten by the exchange (the
-                        // rest of the rows is rewritten by the next predictor's barrier pass)
-                        for (int e = lane; e <= N; e += 64) S.dH[e][C::NDH - 1] = 0.0;
-                        wave_sync();
-                    }
-                    STAMP_LAP(9);
-                    if (own) {
-                        double dxm[NX], dxn[NX], du[NU];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            dxm[i] = k >= 1 ? S.ddz[k][NU + i] : 0.0;
-                            dxn[i] = S.ddz[k + 1][NU + i];
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) du[u] = kf[u];
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) {
-                            double K[NU];
-#pragma unroll
-                            for (int u = NU - 1; u >= 0; --u) {
-                                double acc = -S.Y[k][u][j];
-#pragma unroll
-                                for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * K[m];
-                                K[u] = acc * il[u];
-                            }
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) du[u] += K[u] * dxm[j];
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) S.ddz[k][u] = du[u];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            if (k == 0) S.ddz[0][NU + i] = 0.0;
-                            if constexpr (PIN_SPLIT) continue;
-                            double a = pmine[i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            if constexpr (LEAN) pinr[i] = a;
-                            else S.pin[k][i] = a;
-                        }
-                        if (k == N - 1) {
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) S.ddz[N][u] = 0.0;
-                        }
-                    }
-                    if constexpr (PIN_SPLIT) {
-                        // the new dynamics multipliers, rows split over the parts like the chains' rows
-                        if (k < N) {
-                            double dxn[NX];
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) dxn[i] = S.ddz[k + 1][NU + i];
-#pragma unroll
-                            for (int t = 0; t < RS; ++t) {
-                                if (!rv[t]) continue;
-                                const int i = rs[t];
-                                double a = pmine[i];
-#pragma unroll
-                                for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                                S.pin[k][i] = a;
-                            }
-                        }
-                    }
-                } else
-                {
-                    const bool own = stage_lane && k < N;
-                    const int kq = own ? k : 0;
-                    double Lo[C::NLO > 0 ? C::NLO : 1], il[NU];
-                    if constexpr (NU == 2) {
-                        Lo[0] = S.Lc[kq][1]; il[0] = S.Lc[kq][2]; il[1] = S.Lc[kq][3];
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < C::NLO; ++i) Lo[i] = S.Lc[kq][i];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) il[u] = S.Lc[kq][C::NLO + u];
-                    }
-                    double G[NX][NX], hv[NX], Wu[NU][NX], y0[NU];
-                    double rdv[LEAN ? NX : 1];  // LEAN: recomputed dynamics residual
-                    {
-                        double c[NX], rr[NX];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            if constexpr (LEAN) rr[i] = rdv[i] = rdyn_at(kq, i);
-                            else rr[i] = S.rdyn[kq][i];
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = 0.0;
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += S.P[kq + 1][sym(i, j)] * rr[j];
-                            c[i] = a;
-                        }
-                        double m0[NZ];
-#pragma unroll
-                        for (int i = 0; i < NZ; ++i) {
-                            double a = S.q[kq][i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += Fat(kq, j, i) * c[j];
-                            m0[i] = a;
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            double acc = m0[u];
-#pragma unroll
-                            for (int m = 0; m < u; ++m) acc -= Lo[C::lo_idx(u, m)] * y0[m];
-                            y0[u] = acc * il[u];
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double acc = m0[NU + i];
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) acc -= S.Y[kq][u][i] * y0[u];
-                            hv[i] = acc;
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) {
-                                double w = Fat(kq, i, u);
-#pragma unroll
-                                for (int m = 0; m < u; ++m) w -= Lo[C::lo_idx(u, m)] * Wu[m][i];
-                                Wu[u][i] = w * il[u];
-                            }
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double Yi[NU];
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) Yi[u] = S.Y[kq][u][i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) {
-                                double acc = Fat(kq, j, NU + i);
-#pragma unroll
-                                for (int u = 0; u < NU; ++u) acc -= Yi[u] * Wu[u][j];
-                                G[i][j] = acc;
-                            }
-                        }
-                    }
-                    STAMP_LAP(6);
-                    // each chain step's value is recorded in LDS by the lane that owns it (a
-                    // predicated store off the VALU path) and read back after the chain.  The
-                    // register-starved bicycle instance did the selects into registers until round 4;
-                    // the records keep six doubles per chain out of its registers: scratch 560 -> 504
-                    // B/lane, C3 19.50 -> 18.99 ms (profiles/r04i_ab_*; MPCG_C3_CHAIN_REC=0: A/B)
-#ifndef MPCG_C3_CHAIN_REC
-#define MPCG_C3_CHAIN_REC 1
-#endif
-                    constexpr bool CHAIN_REC = !C::COMPACT || MPCG_C3_CHAIN_REC;
-                    double pu[NX], pmine[NX];
-                    double* const pch = &S.bx[0][0];
-                    static_assert((N + 1) * NZ >= N * NX, "chain storage");
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) { pu[i] = S.q[N][NU + i]; pmine[i] = pu[i]; }
-                    #pragma unroll
-                    for (int kk = N - 1; kk >= 1; --kk) {  // p_0 is not needed
-                        double pn[NX];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = hv[i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += G[i][j] * pu[j];
-                            pn[i] = a;
-                        }
-                        if (CHAIN_REC && lane == kk * PARTS) {
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) pch[kk * NX + i] = pn[i];
-                        }
-                        const bool mine = !CHAIN_REC && (k == kk - 1) && (part == 0);
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            pu[i] = readlane_d(pn[i], kk * PARTS);
-                            if constexpr (!CHAIN_REC) pmine[i] = mine ? pu[i] : pmine[i];
-                        }
-                    }
-                    if constexpr (CHAIN_REC) {
-                        wave_sync();
-                        const double* src = (kq + 1 < N) ? pch + (kq + 1) * NX : &S.q[N][NU];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) pmine[i] = src[i];
-                    }
-                    STAMP_LAP(15);
-                    // feedback of stage k: du = K dx + kff; closed loop dx+ = G' dx + e
-                    double kf[NU];
-                    {
-                        double yy[NU];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            double acc = y0[u];
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) acc += Wu[u][i] * pmine[i];
-                            yy[u] = acc;
-                        }
-#pragma unroll
-                        for (int u = NU - 1; u >= 0; --u) {
-                            double acc = -yy[u];
-#pragma unroll
-                            for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * kf[m];
-                            kf[u] = acc * il[u];
-                        }
-                    }
-                    double e[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        double acc;
-                        if constexpr (LEAN) acc = rdv[i];
-                        else acc = S.rdyn[kq][i];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) acc += Fat(kq, i, u) * kf[u];
-                        e[i] = acc;
-                    }
-                    // dx_{kk+1} goes straight to its place in the QP step, ddz[kk + 1]
-                    double dxu[NX], dxmine[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) { dxu[i] = 0.0; dxmine[i] = 0.0; }
-                    #pragma unroll
-                    for (int kk = 0; kk < N - 1; ++kk) {  // dx_N comes from stage N - 1's own lane
-                        double dn[NX];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = e[i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += G[j][i] * dxu[j];
-                            dn[i] = a;
-                        }
-                        if (CHAIN_REC && lane == kk * PARTS) {
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) S.ddz[kk + 1][NU + i] = dn[i];
-                        }
-                        const bool mine = !CHAIN_REC && (k == kk + 1) && (part == 0);
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            dxu[i] = readlane_d(dn[i], kk * PARTS);
-                            if constexpr (!CHAIN_REC) dxmine[i] = mine ? dxu[i] : dxmine[i];
-                        }
-                    }
-                    if constexpr (CHAIN_REC) {
-                        wave_sync();
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) dxmine[i] = (k >= 1 && k < N) ? S.ddz[k][NU + i] : 0.0;
-                    }
-                    STAMP_LAP(9);
-                    if (own) {
-                        double du[NU], dxn[NX];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) du[u] = kf[u];
-#pragma unroll
-                        for (int j = 0; j < NX; ++j) {
-                            double K[NU];
-#pragma unroll
-                            for (int u = NU - 1; u >= 0; --u) {
-                                double acc = -S.Y[k][u][j];
-#pragma unroll
-                                for (int m = u + 1; m < NU; ++m) acc -= Lo[C::lo_idx(m, u)] * K[m];
-                                K[u] = acc * il[u];
-                            }
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) du[u] += K[u] * dxmine[j];
-                        }
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            double a = e[i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += G[j][i] * dxmine[j];
-                            dxn[i] = a;
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) S.ddz[k][u] = du[u];
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) {
-                            if (!CHAIN_REC || k == 0) S.ddz[k][NU + i] = dxmine[i];  // 0 at k = 0
-                            double a = pmine[i];
-#pragma unroll
-                            for (int j = 0; j < NX; ++j) a += S.P[k + 1][sym(i, j)] * dxn[j];
-                            if constexpr (LEAN) pinr[i] = a;
-                            else S.pin[k][i] = a;
-                        }
-                        if (k == N - 1) {
-#pragma unroll
-                            for (int u = 0; u < NU; ++u) S.ddz[N][u] = 0.0;
-#pragma unroll
-                            for (int i = 0; i < NX; ++i) S.ddz[N][NU + i] = dxn[i];
-                        }
-                    }
-                }
-                wave_sync();
-                STAMP_END(5);
-                // ---- inequality steps, step length, predictor statistics, row update
-                STAMP_BEGIN();
-                {
-                    double ddk[NZ];
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i) ddk[i] = S.ddz[ks][i];
-                    const double smu = sigma_mu;
-                    const int ph = phase;
-                    // per-row D . ddz of the lane's rows
-                    double ddb[BVS];
-#pragma unroll
-                    for (int j = 0; j < BVS; ++j) ddb[j] = LR.box_on(j) ? S.ddz[k][LR.var(j)] : 0.0;
-                    // h rows: D . ddz once per phase (the passes below reuse it)
-                    double ddh[HS];
-#pragma unroll
-                    for (int r = 0; r < HS; ++r) {
-                        double v = 0.0;
-                        if (LR.h_on(r)) {
-                            const int hh = LR.hrow(r);
-                            double ga, gb, gc;
-                            rowg(hh, ga, gb, gc);
-                            v = ga * ddk[X0] + gb * ddk[X1] + gc * ddk[X2];
-                            if constexpr (NB == 4) v += C::slack_coef(hh) * ddk[ZS];
-                        }
-                        ddh[r] = v;
-                    }
-                    auto ddot = [&](int s) {
-                        if (s < HB) return (s & 1) ? ddb[s >> 1] : -ddb[s >> 1];
-                        return ddh[s - HB];
-                    };
-                    auto active = [&](int s) { return s < HB ? LR.box_on(s >> 1) : LR.h_on(s - HB); };
-                    // dt = -rin - D ddz; dl = -(rc + l dt) / t
-                    auto row_step = [&](int s, double& dt, double& dl) {
-                        const double l = R.l[s], t = R.t[s];
-                        const double rc = (ph == 0) ? l * t : l * t + R.pr[s] - smu;
-                        dt = -R.rin[s] - ddot(s);
-                        dl = -(rc + l * dt) * R.it(s);
-                    };
-                    // step to the boundary: min over rows of -t/dt and -l/dl = 1 / max(-dt/t, -dl/l)
-                    // STEP_FORMS: in the predictor rc = l t, so dl = -l (t + dt) / t and a row's
-                    // multiplier blocks (dl < 0) exactly when t + dt > 0, at -dl / l = 1 + dt / t: the row's
-                    // bound is max(-dt/t, 1 + dt/t) (the second term is <= 0 < the first when it does not
-                    // block), no reciprocal of l and no branch; in the corrector the branch on dl < 0 is a
-                    // select (the wave computes the reciprocal whenever any lane needs it)
-#ifndef MPCG_STEP_FORMS
-#define MPCG_STEP_FORMS 1
-#endif
-                    double rmax = 0.0;
-                    if (MPCG_STEP_FORMS && ph == 0) {
-#pragma unroll
-                        for (int s = 0; s < C::SLOTS; ++s) {
-                            if (!active(s)) continue;
-                            double dt, dl;
-                            row_step(s, dt, dl);
-                            const double x = dt * R.it(s);
-                            rmax = fmax(rmax, fmax(-x, 1.0 + x));
-                        }
-                    } else {
-#pragma unroll
-                        for (int s = 0; s < C::SLOTS; ++s) {
-                            if (!active(s)) continue;
-                            double dt, dl;
-                            row_step(s, dt, dl);
-                            rmax = fmax(rmax, -dt * R.it(s));
-                            if (MPCG_STEP_FORMS) {
-                                const double c = -dl * frcp(R.l[s]);
-                                rmax = fmax(rmax, dl < 0.0 ? c : 0.0);
-                            } else if (dl < 0.0) {
-                                rmax = fmax(rmax, -dl * frcp(R.l[s]));
-                            }
-                        }
-                    }
-                    rmax = wave_max(rmax);
-                    const double amax = rmax > 0.0 ? frcp(rmax) : 1e300;
-                    if (phase == 0) {
-                        const double aa = fmin(amax, 1.0);
-                        double ca = 0.0;
-#pragma unroll
-                        for (int s = 0; s < C::SLOTS; ++s) {
-                            if (!active(s)) continue;
-                            double dt, dl;
-                            row_step(s, dt, dl);
-                            ca += (R.l[s] + aa * dl) * (R.t[s] + aa * dt);
-                            R.pr[s] = dt * dl;
-                        }
-                        ca = wave_sum(ca);
-                        const double mu_aff = ca / C::M_TOTAL;
-                        double sig = mu_aff / mu;
-                        if (sig > 1.0) sig = 1.0;
-                        sig = sig * sig * sig;
-                        sigma_mu = sig * mu;
-                    } else {
-                        alpha = 0.995 * amax;
-                        if (alpha > 1.0) alpha = 1.0;
-                        if (alpha >= 1e-12) {
-                            // rows move with the corrector step (rin, ddz of the current iterate), then
-                            // t and lambda are floored at qp_t_min (a compare-select: NaN passes through)
-#pragma unroll
-                            for (int s = 0; s < C::SLOTS; ++s) {
-                                if (!active(s)) continue;
-                                double dt, dl;
-                                row_step(s, dt, dl);
-                                const double tn = R.t[s] + alpha * dt, ln = R.l[s] + alpha * dl;
-                                R.t[s] = tn < tmin ? tmin : tn;
-                                R.l[s] = ln < tmin ? tmin : ln;
-                            }
-                        }
-                    }
-                }
-                wave_sync();
-                STAMP_END(7);
-            }
-            if (qstat == AC_NAN) break;
-            if (alpha < 1e-12) { qstat = AC_MINSTEP; ++qit; break; }
-            // ---- update of the stage variables (rows were updated with the step)
-            STAMP_BEGIN();
-            if (RES_SPLIT && !LEAN) {
-                // every part its variables and dynamics rows (same operations)
-                if (k <= N) {
-#pragma unroll
-                    for (int j = 0; j < BVS; ++j) {
-                        const int v = LR.var(j);
-                        if (v < NZ) S.dz[k][v] += alpha * S.ddz[k][v];
-                    }
-                    if (k < N) {
-#pragma unroll
-                        for (int jd = 0; jd < DRS; ++jd) {
-                            const int i = part + PARTS * jd;
-                            if (i < NX) S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
-                        }
-                    }
-                }
-            } else if (stage_lane) {
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) S.dz[k][i] += alpha * S.ddz[k][i];
-                if (k < N) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        if constexpr (LEAN) S.piq[k][i] += alpha * (pinr[i] - S.piq[k][i]);
-                        else S.piq[k][i] += alpha * (S.pin[k][i] - S.piq[k][i]);
-                    }
-                }
-            }
-            wave_sync();
-            STAMP_END(8);
-        }
-        wave_sync();
-        qp_status = qstat;
-        qp_total += qit;
-        ++sqp_iter;
-        n_maxit += qstat == AC_MAXITER;
-        if (qstat != AC_SUCCESS && qstat != AC_MAXITER) {
-            acados_status = AC_QP_FAILURE;
-            break;
-        }
-        // FIXED_STEP full step on the primal iterate and on every multiplier
-        if (stage_lane) {
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) S.z[k][i] += S.dz[k][i];
-            if (k == N) {
-#pragma unroll
-                for (int u = 0; u < NU; ++u) S.z[N][u] = 0.0;
-            }
-            if (k < N) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) S.pi_nlp[k][i] = S.piq[k][i];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < HS; ++r)
-            if (LR.h_on(r)) R.nlam[r] = R.l[HB + r];
-        wave_sync();
-        acados_status = AC_SUCCESS;
-        // SQP-RTI: the reference's loop stops after a QP that did not succeed
-        // (acados_solver_interface.cpp:105); a full SQP call continues after a max-iter QP
-        if (!sqp_mode && qstat != AC_SUCCESS) break;
-    }
-
-    // ---- completeOneIteration (acados_solver_interface.cpp:162-204)
-    double Lk = 0.0;
-    if (stage_lane && k < N) {
-        double zz[NZ], gd[NZ], Hd[NZ][NZ];
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) zz[i] = S.z[k][i];
-        if constexpr (C::MODEL == 1) Lk = bike::stage_cost(pr, pk, k, zz, gd, Hd, false);
-        else Lk = stage_cost<NX>(pr, pk, zz, gd, Hd, false);
-    }
-    const double pobj = wave_sum(Lk);
-    double* xo = io.xtraj + (size_t)sol * (N + 1) * NX;
-    for (int e = lane; e < (N + 1) * NX; e += 64) xo[e] = S.z[e / NX][NU + e % NX];
-    double* uo = io.utraj + (size_t)sol * N * NU;
-    for (int e = lane; e < N * NU; e += 64) uo[e] = S.z[e / NU][e % NU];
-    if (io.lam_out) {
-        double* lo = io.lam_out + (size_t)sol * N * LAMS;
-        for (int e = lane; e < N * NX; e += 64) lo[(size_t)(e / NX) * LAMS + e % NX] = S.pi_nlp[e / NX][e % NX];
-        if (k == 0) {
-            for (int r = part; r < C::NH; r += PARTS) lo[NX + r] = 0.0;
-        } else if (k < N) {
-#pragma unroll
-            for (int r = 0; r < HS; ++r)
-                if (LR.h_on(r)) lo[(size_t)k * LAMS + NX + LR.hrow(r)] = R.nlam[r];
-        }
-    }
-    if (FULL && io.qp_out) {
-        double* q = io.qp_out + (size_t)sol * C::QPM;
-#pragma unroll
-        for (int sl = 0; sl < C::SLOTS; ++sl) {
-            q[(2 * sl) * 64 + lane] = R.t[sl];
-            q[(2 * sl + 1) * 64 + lane] = R.l[sl];
-        }
-        for (int e = lane; e < (N + 1) * NZ; e += 64) q[C::QPM_ROWS + e] = (&S.dz[0][0])[e];
-        for (int e = lane; e < N * NX; e += 64) q[C::QPM_ROWS + (N + 1) * NZ + e] = (&S.piq[0][0])[e];
-    }
-    if (FULL && io.stats && lane == 0) {
-        double* st = io.stats + (size_t)sol * MPCG_STATS_STRIDE;
-        st[0] = nlp_stat;
-        st[1] = res_eq;
-        st[2] = nlp_ineq;
-        st[3] = nlp_comp;
-    }
-    if (lane == 0) {
-        int code = acados_status;
-        if (res_eq > pr.res_eq_fail && code == AC_SUCCESS) code = AC_QP_FAILURE;
-        if (code == AC_SUCCESS) code = 1;
-        else if (code == 1) code = 0;
-        io.exit_code[sol] = code;
-        io.pobj[sol] = pobj;
-        if (io.info) {
-            io.info[(size_t)sol * MPCG_INFO_STRIDE + 0] = sqp_iter;
-            io.info[(size_t)sol * MPCG_INFO_STRIDE + 1] = qp_total;
-            io.info[(size_t)sol * MPCG_INFO_STRIDE + 2] = qp_status;
-            io.info[(size_t)sol * MPCG_INFO_STRIDE + 3] = n_maxit;
-        }
-    }
-    STAMP_STORE(stamps, sol);
+#include "mpcg_sqp_body.inc"
 }
 
 // The batched solve.  queue == NULL or an instance without C::QUEUE: workgroup b solves problem b
@@ -2746,7 +675,8 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
                                                     double* __restrict__ gws, unsigned* __restrict__ queue) {
     if constexpr (!C::QUEUE) {
         (void)queue;
-        sqp_solve<C, FULL>(pr, batch, io, stamps, gws, blockIdx.x);
+        const int sol = blockIdx.x;
+#include "mpcg_sqp_body.inc"
     } else {
         if (blockDim.x != 64) {
             // the lane exchanges assume one wavefront per workgroup (wave_sync): any other launch
