@@ -37,7 +37,7 @@ struct SolverConfig {
     // <solver dir>/<name>.yaml
     static std::string solverFile(const std::string& name);
     // the planner settings (the reference's CONFIG), loaded once
-    static const mpcg::YamlNode& settings();
+    static const YamlNode& settings();
     static void reload();
 };
 

@@ -35,7 +35,7 @@ struct AcadosParameters {
     double* getU0() { return x0; }
 
     AcadosParameters();
-    void printParameters(const mpcg::YamlNode& parameter_map) const;
+    void printParameters(const YamlNode& parameter_map) const;
 };
 
 class Solver {
@@ -85,7 +85,7 @@ public:
     unsigned int npar;
     double dt;
 
-    mpcg::YamlNode _config, _parameter_map, _model_map;
+    YamlNode _config, _parameter_map, _model_map;
 
     int _num_iterations;
 

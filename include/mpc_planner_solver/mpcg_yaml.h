@@ -81,3 +81,22 @@ YamlNode yaml_parse(const std::string& text);
 YamlNode yaml_load_file(const std::string& path);
 
 }  // namespace mpcg
+
+// The node type of the Solver's public _config / _parameter_map / _model_map (the reference's are
+// YAML::Node, acados_solver_interface.h:175, state.h:29): yaml-cpp's own where it is on the include
+// path, so reference code that hands these members to yaml-cpp links unchanged; this reader's
+// otherwise (same access API).  -DMPCG_NO_YAML_CPP keeps this reader with yaml-cpp present.
+#if __has_include(<yaml-cpp/yaml.h>) && !defined(MPCG_NO_YAML_CPP)
+#include <yaml-cpp/yaml.h>
+#define MPCG_YAML_CPP 1
+namespace MPCPlanner {
+using YamlNode = YAML::Node;
+inline YamlNode load_yaml_file(const std::string& path) { return YAML::LoadFile(path); }
+}  // namespace MPCPlanner
+#else
+#define MPCG_YAML_CPP 0
+namespace MPCPlanner {
+using YamlNode = mpcg::YamlNode;
+inline YamlNode load_yaml_file(const std::string& path) { return mpcg::yaml_load_file(path); }
+}  // namespace MPCPlanner
+#endif

@@ -28,7 +28,7 @@ struct State {
 
 private:
     std::vector<double> _state;
-    mpcg::YamlNode _config, _model_map;
+    YamlNode _config, _model_map;
     int _nu = 0;
     int index(const std::string& var_name) const;
 };

@@ -37,7 +37,7 @@ extern "C" {
 #define MPCG_NU 2            /* the unicycle models */
 #define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 7
+#define MPCG_ABI_VERSION 8
 /* mpcg_problem.model */
 #define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
 #define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
@@ -103,9 +103,29 @@ typedef struct mpcg_problem {
                                       the dual-degenerate SH-MPC QPs' exit decisions stop depending on rounding,
                                       DESIGN.md §2.2); 0 = no floor */
     double qp_mu_max;              /* divergence test: an interior point whose mean complementarity reaches this
-                                      (1e8: 1e8 x the cold start's) is diverging -- the QP is infeasible, its duals
-                                      blow up -- and ends with the NaN status */
+                                      is diverging -- the QP is infeasible, its duals blow up -- and ends with the
+                                      NaN status (robust profile: 1e8; <= 0: no such test, HPIPM's behaviour, where
+                                      only a non-finite iterate ends a QP with that status) */
+    /* ABI 8: the interior point's profile (mpcg_problem_set_qp_profile sets the group).
+     * MPCG_QP_HPIPM (the default of mpcg_problem_from_map*): HPIPM's BALANCE mode as acados configures it,
+     * which the reference leaves at acados' defaults but for four options (generate_acados_solver.py:162-173):
+     * qp_mu0 10, qp_thr0 0.1, qp_t_min 1e-16, qp_mu_max 0 and 1 / 1 / 2 / 0 / 1 below.  MPCG_QP_ROBUST:
+     * the round-4 algorithm, qp_mu0 1, qp_thr0 1, qp_t_min 1e-12, qp_mu_max 1e8 and 0 / 0 / 0 / 1 / 0. */
+    int qp_profile;                /* MPCG_QP_*: what mpcg_problem_set_qp_profile wrote (informative) */
+    int qp_init_move;              /* HPIPM init_var at a cold start: a box row whose gap is below qp_thr0 moves
+                                      the primal start inside its bounds (to the midpoint when both are) */
+    int qp_cond_pred_corr;         /* conditional predictor-corrector: a centring direction when the corrected
+                                      one's mu_aff exceeds twice the predictor's */
+    int qp_itref_corr_max;         /* iterative refinement steps of the corrector direction (its linear KKT
+                                      residual above max(qp_tol, 1e-3 x the iterate's residual)) */
+    int qp_sigma_clip;             /* 1: sigma = min(mu_aff / mu, 1)^3; 0: (mu_aff / mu)^3 (HPIPM) */
+    int qp_maxit_first;            /* 1: the iteration cap is tested before convergence (HPIPM's exit order) */
 } mpcg_problem;
+
+#define MPCG_QP_HPIPM 0
+#define MPCG_QP_ROBUST 1
+/* Set the interior point's profile fields of `pr` (above).  Returns 0, or -1 for an unknown profile. */
+int mpcg_problem_set_qp_profile(mpcg_problem *pr, int profile);
 
 /* per-solve diagnostics, int32 x 4: sqp iterations, total QP iterations,
  * last QP status (acados: 0 ok, 1 nan/diverged, 2 max-iter, 3 min-step), and the

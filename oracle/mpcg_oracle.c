@@ -548,6 +548,11 @@ typedef struct {
     double il[NU];  /* reciprocal pivots 1/L_ii (default build, nu 2) */
     double Hh[NZ][NZ], q[NZ];
     double dz[NZ], ddz[NZ], pi[NX], pin[NX];
+    /* iterative refinement (qp_itref_corr_max): the iterate's stationarity residual, the
+     * linear KKT residual of the step (stationarity, dynamics; rows in ld / lm) and the
+     * unrefined step */
+    double rg[NZ], lg[NZ], lb[NX], ddz0[NZ], pin0[NX];
+    double *ld, *lm;
 } qp_stage;
 
 typedef struct {
@@ -556,9 +561,9 @@ typedef struct {
 } qp_ws;
 
 /* stationarity residual of stage k on its free variables */
-static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *mu, int *mtot) {
+static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *mu, int *mtot, double *cmx) {
     int N = w->N;
-    double s_max = 0.0, e_max = 0.0, i_max = 0.0, comp = 0.0;
+    double s_max = 0.0, e_max = 0.0, i_max = 0.0, comp = 0.0, c_max = 0.0;
     int m = 0;
     for (int k = 0; k <= N; k++) {
         qp_stage *S = &w->st[k];
@@ -593,6 +598,7 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
             S->rin[c] = acc;
             if (fabs(acc) > i_max) i_max = fabs(acc);
             comp += S->lam[c] * S->t[c];
+            if (fabs(S->lam[c] * S->t[c]) > c_max) c_max = fabs(S->lam[c] * S->t[c]);
             m++;
         }
         if (KF) {
@@ -652,6 +658,18 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
         int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
         for (int i = i0; i < i1; i++)
             if (fabs(r[i]) > s_max) s_max = fabs(r[i]);
+        memcpy(S->rg, r, sizeof r);
+        if (getenv("ORC_DEBUG3")) {
+            for (int i = i0; i < i1; i++) {
+                if (fabs(r[i]) < 1e-7) continue;
+                double hz = 0.0, dl = 0.0, fp = 0.0, bx = 0.0, mx = 0.0;
+                for (int j = 0; j < NZ; j++) hz += S->H[i][j] * S->dz[j];
+                for (int c = 0; c < S->ni; c++) { double v = S->D[c][i] * S->lam[c]; if (S->hrow[c] < 0) bx += v; else dl += v; if (fabs(v) > mx) mx = fabs(v); }
+                if (k < N) for (int m2 = 0; m2 < NX; m2++) fp += (i < NU ? S->B[m2][i] : S->A[m2][i - NU]) * S->pi[m2];
+                double pp = (k > 0 && i >= NU) ? w->st[k - 1].pi[i - NU] : 0.0;
+                fprintf(stderr, "      k %d var %d r %.3e | Hdz %.6e g %.6e box %.6e hrows %.6e (max term %.3e) Fpi %.6e pprev %.6e\n", k, i, r[i], hz, S->g[i], bx, dl, mx, fp, pp);
+            }
+        }
         if (k < N) {
             qp_stage *S1 = &w->st[k + 1];
             for (int i = 0; i < NX; i++) {
@@ -665,6 +683,7 @@ static void qp_residuals(qp_ws *w, double *rs, double *re, double *ri, double *m
     *rs = s_max; *re = e_max; *ri = i_max;
     *mtot = m;
     *mu = m ? comp / m : 0.0;
+    *cmx = c_max;
 }
 
 /* dynamics residual r_k = A dx_k + B du_k + b_k - dx_{k+1} */
@@ -765,10 +784,16 @@ static int riccati_factor(qp_ws *w) {
 /* vector pass + forward substitution for gradient q (in S->q) and the
  * current dynamics residuals; writes ddz (step) and pin (new dynamics
  * multipliers) */
+static void riccati_solve_r(qp_ws *w, double (*r)[NX]);
 static void riccati_solve(qp_ws *w) {
-    int N = w->N;
     double r[ORC_MAX_N][NX];
-    for (int k = 0; k < N; k++) dyn_res(w, k, r[k]);
+    for (int k = 0; k < w->N; k++) dyn_res(w, k, r[k]);
+    riccati_solve_r(w, r);
+}
+
+/* the same for the dynamics right-hand sides r (the iterative refinement's) */
+static void riccati_solve_r(qp_ws *w, double (*r)[NX]) {
+    int N = w->N;
     qp_stage *SN = &w->st[N];
     for (int i = 0; i < NX; i++) SN->p[i] = SN->q[NU + i];
     for (int k = N - 1; k >= 0; k--) {
@@ -886,19 +911,106 @@ static double max_step(qp_ws *w) {
     return amax;
 }
 
-static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
+/* linear residual of the Newton system for the step (ddz, pin - pi, dt, dl) against its
+ * right-hand side (the iterate's rg, dynamics residual, rin, rc) -- HPIPM res_compute_lin --
+ * into lg / lb / ld / lm; res[0..3] = inf-norms (stationarity on the free variables, dynamics,
+ * rows, complementarity) */
+static void lin_residuals(qp_ws *w, double res[4]) {
+    int N = w->N;
+    res[0] = res[1] = res[2] = res[3] = 0.0;
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w->st[k];
+        double r[NZ];
+        for (int i = 0; i < NZ; i++) {
+            double acc = S->rg[i];
+            for (int j = 0; j < NZ; j++) acc += S->H[i][j] * S->ddz[j];
+            r[i] = acc;
+        }
+        for (int c = 0; c < S->ni; c++) {
+            for (int i = 0; i < NZ; i++) r[i] += S->D[c][i] * S->dl[c];
+            double dd = 0.0;
+            for (int i = 0; i < NZ; i++) dd += S->D[c][i] * S->ddz[i];
+            S->ld[c] = S->rin[c] + dd + S->dt[c];
+            S->lm[c] = S->rc[c] + S->lam[c] * S->dt[c] + S->t[c] * S->dl[c];
+            if (fabs(S->ld[c]) > res[2] || isnan(S->ld[c])) res[2] = fabs(S->ld[c]);
+            if (fabs(S->lm[c]) > res[3] || isnan(S->lm[c])) res[3] = fabs(S->lm[c]);
+        }
+        if (k < N)
+            for (int i = 0; i < NZ; i++)
+                for (int m = 0; m < NX; m++)
+                    r[i] += (i < NU ? S->B[m][i] : S->A[m][i - NU]) * (S->pin[m] - S->pi[m]);
+        if (k > 0)
+            for (int i = 0; i < NX; i++) r[NU + i] -= w->st[k - 1].pin[i] - w->st[k - 1].pi[i];
+        int i0 = (k == N) ? NU : 0, i1 = (k == 0) ? NU : NZ;
+        for (int i = 0; i < NZ; i++) S->lg[i] = (i >= i0 && i < i1) ? r[i] : 0.0;
+        for (int i = i0; i < i1; i++)
+            if (fabs(r[i]) > res[0] || isnan(r[i])) res[0] = fabs(r[i]);
+        if (k < N) {
+            qp_stage *S1 = &w->st[k + 1];
+            double rb[NX];
+            dyn_res(w, k, rb);
+            for (int i = 0; i < NX; i++) {
+                double acc = rb[i] - S1->ddz[NU + i];
+                for (int j = 0; j < NX; j++) acc += S->A[i][j] * S->ddz[NU + j];
+                for (int j = 0; j < NU; j++) acc += S->B[i][j] * S->ddz[j];
+                S->lb[i] = acc;
+                if (fabs(acc) > res[1] || isnan(acc)) res[1] = fabs(acc);
+            }
+        }
+    }
+}
+
+static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm, int *n_center, int *n_itref) {
     int N = w->N;
     if (!warm) {
-        /* cold start */
+        /* cold start (HPIPM init_var, warm_start 0): ux = 0, pi = 0; then per row t = gap at
+         * ux clipped below at thr0, lambda = mu0 / t.  With qp_init_move (HPIPM's own start), the
+         * box rows come first: a variable whose lower (upper) gap is below thr0 is moved to
+         * thr0 inside that bound, or to the midpoint of its bounds when both gaps are; the
+         * general rows then take their gaps at the moved ux */
+        const double thr0 = pr->qp_thr0;
         for (int k = 0; k <= N; k++) {
             qp_stage *S = &w->st[k];
             for (int i = 0; i < NZ; i++)
                 if (!(k == 0 && i >= NU)) S->dz[i] = 0.0; /* x0 part stays fixed */
             for (int i = 0; i < NX; i++) S->pi[i] = 0.0;
-            for (int c = 0; c < S->ni; c++) {
-                double s = S->d[c];
-                for (int i = 0; i < NZ; i++) s -= S->D[c][i] * S->dz[i];
-                S->t[c] = s > pr->qp_thr0 ? s : pr->qp_thr0;
+            int c0 = 0;
+            if (pr->qp_init_move) {
+                /* box rows: pairs (lower, upper) of one variable, before the h rows (linearise) */
+                for (; c0 + 1 < S->ni && S->hrow[c0] < 0; c0 += 2) {
+                    int v = 0;
+                    while (v < NZ && S->D[c0][v] == 0.0) v++;
+                    double tl = S->d[c0] + S->dz[v], tu = S->d[c0 + 1] - S->dz[v]; /* -d_lb + ux, d_ub - ux */
+                    if (tl < thr0) {
+                        if (tu < thr0) {
+                            S->dz[v] = 0.5 * (-S->d[c0] + S->d[c0 + 1]); /* 0.5 (d_lb + d_ub) */
+                            tl = thr0;
+                            tu = thr0;
+                        } else {
+                            tl = thr0;
+                            S->dz[v] = -S->d[c0] + thr0; /* d_lb + thr0 */
+                        }
+                    } else if (tu < thr0) {
+                        tu = thr0;
+                        S->dz[v] = S->d[c0 + 1] - thr0; /* d_ub - thr0 */
+                    }
+                    S->t[c0] = tl;
+                    S->t[c0 + 1] = tu;
+                    S->lam[c0] = pr->qp_mu0 / tl;
+                    S->lam[c0 + 1] = pr->qp_mu0 / tu;
+                }
+            }
+            for (int c = c0; c < S->ni; c++) {
+                double s;
+                if (pr->qp_init_move) {
+                    double dd = 0.0; /* t = -D ux + d (HPIPM's order) */
+                    for (int i = 0; i < NZ; i++) dd += S->D[c][i] * S->dz[i];
+                    s = -dd + S->d[c];
+                } else {
+                    s = S->d[c];
+                    for (int i = 0; i < NZ; i++) s -= S->D[c][i] * S->dz[i];
+                }
+                S->t[c] = s > thr0 ? s : thr0;
                 S->lam[c] = pr->qp_mu0 / S->t[c];
             }
         }
@@ -918,12 +1030,17 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
     }
     int status = AC_MAXITER;
     int it;
+    /* the divergence test of the robust profile (qp_mu_max > 0); without it only a non-finite
+     * mu ends the QP with the NaN status */
+    const double mu_lim = pr->qp_mu_max > 0.0 ? pr->qp_mu_max : INFINITY;
     for (it = 0;; it++) {
-        double rs, re, ri, mu;
+        double rs, re, ri, mu, cmx;
         int m;
-        qp_residuals(w, &rs, &re, &ri, &mu, &m);
+        qp_residuals(w, &rs, &re, &ri, &mu, &m, &cmx);
         /* non-finite or diverged (infeasible QP: duals blow up; qp_mu_max) -> NaN status */
-        if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < pr->qp_mu_max)) { status = AC_NAN; break; }
+        if (!(rs < 1e30) || !(re < 1e30) || !(ri < 1e30) || !(mu < mu_lim)) { status = AC_NAN; break; }
+        /* HPIPM's exit order: the iteration cap first (qp_maxit_first) */
+        if (pr->qp_maxit_first && it >= pr->qp_iter_max) { status = AC_MAXITER; break; }
         if (getenv("ORC_DEBUG")) fprintf(stderr, "  ipm it %d rs %.3e re %.3e ri %.3e mu %.3e\n", it, rs, re, ri, mu);
         if (getenv("ORC_DEBUG2")) {
             /* top complementarity contributors */
@@ -970,7 +1087,7 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
         }
         double mu_aff = comp_aff / m;
         double sig = mu_aff / mu;
-        if (sig > 1.0) sig = 1.0;
+        if (pr->qp_sigma_clip && sig > 1.0) sig = 1.0;
         sig = sig * sig * sig;
         /* corrector */
         for (int k = 0; k <= N; k++) {
@@ -981,6 +1098,83 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm) {
         build_q(w);
         riccati_solve(w);
         ineq_steps(w, NULL);
+        if (pr->qp_cond_pred_corr) {
+            /* HPIPM cond_pred_corr: mu_aff of the corrected direction (its boundary step, at most
+             * 1); above twice the predictor's, the direction is the centring one instead
+             * (complementarity target sigma mu without the second-order term) */
+            double ac = max_step(w);
+            if (ac > 1.0) ac = 1.0;
+            double cc = 0.0;
+            if (KK) {
+                /* kernel forms: sum l t + a (sum (l dt + t dl) + a sum dl dt) */
+                double cb = 0.0, cq = 0.0;
+                for (int k = 0; k <= N; k++) {
+                    qp_stage *S = &w->st[k];
+                    for (int c = 0; c < S->ni; c++) {
+                        cb += S->lam[c] * S->dt[c] + S->t[c] * S->dl[c];
+                        cq += S->dl[c] * S->dt[c];
+                    }
+                }
+                cc = mu * m + ac * (cb + ac * cq);
+            } else {
+                for (int k = 0; k <= N; k++) {
+                    qp_stage *S = &w->st[k];
+                    for (int c = 0; c < S->ni; c++) cc += (S->lam[c] + ac * S->dl[c]) * (S->t[c] + ac * S->dt[c]);
+                }
+            }
+            if (cc / m > 2.0 * mu_aff) {
+                for (int k = 0; k <= N; k++) {
+                    qp_stage *S = &w->st[k];
+                    for (int c = 0; c < S->ni; c++) S->rc[c] = S->lam[c] * S->t[c] - sig * mu;
+                }
+                build_q(w);
+                riccati_solve(w);
+                ineq_steps(w, NULL);
+                ++*n_center;
+            }
+        }
+        /* HPIPM itref_corr_max: while the direction's linear KKT residual is not below
+         * max(tol, 1e-3 x the iterate's residual) in every component, solve the Newton system
+         * again for it (same factorisation) and add the correction; dt and dl then follow from
+         * the refined step */
+        for (int itr = 0; itr < pr->qp_itref_corr_max; itr++) {
+            double lr[4];
+            lin_residuals(w, lr);
+            const double tol = pr->qp_tol;
+            const int pass_ = (lr[0] < tol || lr[0] < 1e-3 * rs) && (lr[1] < tol || lr[1] < 1e-3 * re) &&
+                (lr[2] < tol || lr[2] < 1e-3 * ri) && (lr[3] < tol || lr[3] < 1e-3 * cmx);
+            if (getenv("ORC_ITREF_DIAG")) {
+                double lmx = 0, itm = 0, dlm = 0, pmx = 0, dzm = 0;
+                for (int k = 0; k <= N; k++) { qp_stage *S = &w->st[k];
+                    for (int c = 0; c < S->ni; c++) { if (S->lam[c] > lmx) lmx = S->lam[c]; if (1.0/S->t[c] > itm) itm = 1.0/S->t[c]; if (fabs(S->dl[c]) > dlm) dlm = fabs(S->dl[c]); }
+                    for (int i = 0; i < NX; i++) for (int j = 0; j < NX; j++) if (fabs(S->P[i][j]) > pmx) pmx = fabs(S->P[i][j]);
+                    for (int i = 0; i < NZ; i++) if (fabs(S->ddz[i]) > dzm) dzm = fabs(S->ddz[i]); }
+                fprintf(stderr, "ITREF %d itr %d lam %.2e it %.2e dl %.2e P %.2e dz %.2e | lr %.1e %.1e %.1e %.1e | r %.1e %.1e %.1e %.1e\n", pass_, itr, lmx, itm, dlm, pmx, dzm, lr[0], lr[1], lr[2], lr[3], rs, re, ri, cmx);
+            }
+            if (pass_) break;
+            double rb[ORC_MAX_N][NX];
+            for (int k = 0; k <= N; k++) {
+                qp_stage *S = &w->st[k];
+                memcpy(S->ddz0, S->ddz, sizeof S->ddz);
+                memcpy(S->pin0, S->pin, sizeof S->pin);
+                if (k < N) memcpy(rb[k], S->lb, sizeof S->lb);
+                for (int i = 0; i < NZ; i++) S->q[i] = S->lg[i];
+                for (int c = 0; c < S->ni; c++) {
+                    const double coef = KF ? (S->lam[c] * S->ld[c] - S->lm[c]) * (1.0 / S->t[c])
+                                           : (S->lam[c] * S->ld[c] - S->lm[c]) / S->t[c];
+                    for (int i = 0; i < NZ; i++) S->q[i] += S->D[c][i] * coef;
+                }
+            }
+            riccati_solve_r(w, rb);
+            for (int k = 0; k <= N; k++) {
+                qp_stage *S = &w->st[k];
+                for (int i = 0; i < NZ; i++) S->ddz[i] = S->ddz0[i] + S->ddz[i];
+                if (k < N)
+                    for (int i = 0; i < NX; i++) S->pin[i] = S->pin0[i] + S->pin[i];
+            }
+            ineq_steps(w, NULL);
+            ++*n_itref;
+        }
         double alpha = 0.995 * max_step(w);
         if (alpha > 1.0) alpha = 1.0;
         if (alpha < 1e-12) { status = AC_MINSTEP; it++; break; }
@@ -1155,7 +1349,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
     w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
     size_t nrow = (size_t)(N + 1) * maxi;
     double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));
-    double *dbl = (double *)calloc(nrow * 9, sizeof(double));
+    double *dbl = (double *)calloc(nrow * 11, sizeof(double));
     int *ibl = (int *)calloc(nrow * 2, sizeof(int));
     for (int k = 0; k <= N; k++) {
         qp_stage *S = &w.st[k];
@@ -1164,6 +1358,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
         S->d = dbl + o; S->t = dbl + nrow + o; S->lam = dbl + 2 * nrow + o;
         S->dt = dbl + 3 * nrow + o; S->dl = dbl + 4 * nrow + o; S->dt_aff = dbl + 5 * nrow + o;
         S->dl_aff = dbl + 6 * nrow + o; S->rin = dbl + 7 * nrow + o; S->rc = dbl + 8 * nrow + o;
+        S->ld = dbl + 9 * nrow + o; S->lm = dbl + 10 * nrow + o;
         S->hrow = ibl + o; S->hsgn = ibl + nrow + o;
     }
     /* NLP iterate: z_k = [u_k; x_k] from the warm start (loadWarmstart, acados_solver_interface.cpp:274-284);
@@ -1205,6 +1400,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
 
     double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0, n_maxit = 0;
+    int n_center = 0, n_itref = 0;
     double res_eq = 0.0;
 
     const int sqp_mode = pr->nlp_solver == 1;
@@ -1245,7 +1441,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
          * the first with warm_start_first_qp) */
         int qit = 0;
         const int warm = have_qp && pr->qp_warm_start == 2 && ((sqp_mode && it > 0) || pr->qp_warm_first);
-        qp_status = qp_solve(pr, &w, &qit, warm);
+        qp_status = qp_solve(pr, &w, &qit, warm, &n_center, &n_itref);
         have_qp = 1;
         qp_iter_total += qit;
         sqp_iter++;
@@ -1315,6 +1511,8 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
         info->res_ineq = res_ineq;
         info->res_comp = res_comp;
         info->qp_maxiter = n_maxit;
+        info->qp_center = n_center;
+        info->qp_itref = n_itref;
     }
     free(hh); free(lamh); free(pi); free(z);
     free(ibl); free(dbl); free(Dall); free(w.st);
@@ -1398,7 +1596,7 @@ int orc_qp_data(const orc_problem *pr, const double *params, const double *warm,
     w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
     size_t nrow = (size_t)(N + 1) * maxi;
     double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));
-    double *dbl = (double *)calloc(nrow * 9, sizeof(double));
+    double *dbl = (double *)calloc(nrow * 11, sizeof(double));
     int *ibl = (int *)calloc(nrow * 2, sizeof(int));
     for (int k = 0; k <= N; k++) {
         qp_stage *S = &w.st[k];
@@ -1407,6 +1605,7 @@ int orc_qp_data(const orc_problem *pr, const double *params, const double *warm,
         S->d = dbl + o; S->t = dbl + nrow + o; S->lam = dbl + 2 * nrow + o;
         S->dt = dbl + 3 * nrow + o; S->dl = dbl + 4 * nrow + o; S->dt_aff = dbl + 5 * nrow + o;
         S->dl_aff = dbl + 6 * nrow + o; S->rin = dbl + 7 * nrow + o; S->rc = dbl + 8 * nrow + o;
+        S->ld = dbl + 9 * nrow + o; S->lm = dbl + 10 * nrow + o;
         S->hrow = ibl + o; S->hsgn = ibl + nrow + o;
     }
     double (*z)[NZ] = (double (*)[NZ])calloc(N + 1, sizeof(double[NZ]));

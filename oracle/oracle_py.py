@@ -32,6 +32,17 @@ for _m, _stem in (("unicycle", "libmpcg_oracle"), ("unicycle_slack", "libmpcg_or
 
 ORC_MAX_NU, ORC_MAX_NX = 3, 6
 
+# The interior point's profiles (the same values as the product's
+# mpcg_problem_set_qp_profile): "hpipm" restates HPIPM's BALANCE mode as acados configures it
+# (the reference leaves every QP option but four at acados' defaults,
+# generate_acados_solver.py:162-173), "robust" is round 4's algorithm.
+QP_PROFILES = {
+    "hpipm": dict(qp_mu0=10.0, qp_thr0=0.1, qp_t_min=1e-16, qp_mu_max=0.0, qp_init_move=1, qp_cond_pred_corr=1,
+                  qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1),
+    "robust": dict(qp_mu0=1.0, qp_thr0=1.0, qp_t_min=1e-12, qp_mu_max=1e8, qp_init_move=0, qp_cond_pred_corr=0,
+                   qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0),
+}
+
 
 class OrcProblem(C.Structure):
     _fields_ = [
@@ -55,6 +66,8 @@ class OrcProblem(C.Structure):
         ("qp_warm_start", C.c_int), ("qp_ws_thr", C.c_double),
         ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
         ("qp_t_min", C.c_double), ("qp_mu_max", C.c_double),
+        ("qp_init_move", C.c_int), ("qp_cond_pred_corr", C.c_int), ("qp_itref_corr_max", C.c_int),
+        ("qp_sigma_clip", C.c_int), ("qp_maxit_first", C.c_int),
     ]
 
 
@@ -62,7 +75,7 @@ class OrcInfo(C.Structure):
     _fields_ = [("sqp_iter", C.c_int), ("qp_iter_total", C.c_int), ("qp_status", C.c_int),
                 ("res_eq", C.c_double), ("pobj", C.c_double),
                 ("res_stat", C.c_double), ("res_ineq", C.c_double), ("res_comp", C.c_double),
-                ("qp_maxiter", C.c_int)]
+                ("qp_maxiter", C.c_int), ("qp_center", C.c_int), ("qp_itref", C.c_int)]
 
 
 def build(force: bool = False) -> str:
@@ -137,8 +150,9 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.qp_tol = opts.get("qp_tol", 1e-5)
     pr.qp_iter_max = opts.get("qp_iter_max", 50)
     pr.reg_eps = opts.get("reg_eps", 1e-4)
-    pr.qp_mu0 = opts.get("qp_mu0", 1.0)
-    pr.qp_thr0 = opts.get("qp_thr0", 1.0)
+    prof = QP_PROFILES[opts.get("qp_profile", "hpipm")]
+    pr.qp_mu0 = opts.get("qp_mu0", prof["qp_mu0"])
+    pr.qp_thr0 = opts.get("qp_thr0", prof["qp_thr0"])
     pr.res_eq_fail = opts.get("res_eq_fail", 1e-2)
     # QP start as the reference configures it: qp_solver_warm_start 2 (generate_acados_solver.py:173)
     # with warm_start_first_qp off -- every SQP-RTI QP starts cold; qp_warm_first=1 warm-starts the
@@ -150,10 +164,11 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     pr.nlp_solver = {"SQP_RTI": 0, "SQP": 1}[opts.get("solver_type", "SQP_RTI")]
     pr.nlp_max_iter = opts.get("nlp_max_iter", 100)
     pr.nlp_tol = opts.get("nlp_tol", 1e-2)
-    # floor of t and lambda after every interior-point step
-    pr.qp_t_min = opts.get("qp_t_min", 1e-12)
-    # divergence test of the interior point
-    pr.qp_mu_max = opts.get("qp_mu_max", 1e8)
+    # floor of t and lambda after every interior-point step, the divergence test (<= 0: none) and
+    # the structural switches of the profile
+    for f in ("qp_t_min", "qp_mu_max", "qp_init_move", "qp_cond_pred_corr", "qp_itref_corr_max", "qp_sigma_clip",
+              "qp_maxit_first"):
+        setattr(pr, f, opts.get(f, prof[f]))
     return pr
 
 
@@ -299,7 +314,8 @@ class Oracle:
                    sqp_iter=get("sqp_iter", np.int32), qp_status=get("qp_status", np.int32),
                    res_eq=get("res_eq", float), res_stat=get("res_stat", float),
                    res_ineq=get("res_ineq", float), res_comp=get("res_comp", float),
-                   qp_maxiter=get("qp_maxiter", np.int32))
+                   qp_maxiter=get("qp_maxiter", np.int32), qp_center=get("qp_center", np.int32),
+                   qp_itref=get("qp_itref", np.int32))
         if return_lam:
             out["lam"] = lo
         if return_qp:

@@ -20,7 +20,7 @@ namespace {
 std::mutex g_cfg_mutex;
 std::string g_solver_dir, g_settings_file;
 bool g_settings_loaded = false;
-mpcg::YamlNode g_settings;
+YamlNode g_settings;
 
 std::string env_or(const char* name, const std::string& fallback) {
     const char* v = std::getenv(name);
@@ -52,12 +52,12 @@ std::string SolverConfig::solverDirectory() {
 
 std::string SolverConfig::solverFile(const std::string& name) { return solverDirectory() + "/" + name + ".yaml"; }
 
-const mpcg::YamlNode& SolverConfig::settings() {
+const YamlNode& SolverConfig::settings() {
     std::lock_guard<std::mutex> l(g_cfg_mutex);
     if (!g_settings_loaded) {
         std::string f = g_settings_file.empty() ? env_or("MPCG_SETTINGS", "") : g_settings_file;
         if (f.empty()) fatal("no planner settings: SolverConfig::setSettingsFile() or MPCG_SETTINGS");
-        g_settings = mpcg::yaml_load_file(f);
+        g_settings = load_yaml_file(f);
         g_settings_loaded = true;
     }
     return g_settings;
@@ -70,8 +70,8 @@ void SolverConfig::reload() {
 
 // -------------------------------------------------------------------- State
 State::State() {
-    _config = mpcg::yaml_load_file(SolverConfig::solverFile("solver_settings"));
-    _model_map = mpcg::yaml_load_file(SolverConfig::solverFile("model_map"));
+    _config = load_yaml_file(SolverConfig::solverFile("solver_settings"));
+    _model_map = load_yaml_file(SolverConfig::solverFile("model_map"));
     initialize();
 }
 
@@ -81,7 +81,7 @@ void State::initialize() {
 }
 
 int State::index(const std::string& var_name) const {
-    const mpcg::YamlNode& e = _model_map[var_name];
+    const YamlNode& e = _model_map[var_name];
     if (!e.IsDefined()) throw std::runtime_error("State: no variable '" + var_name + "' in model_map.yaml");
     return e[1].as<int>() - _nu;  // states come after the inputs
 }
@@ -111,7 +111,7 @@ AcadosParameters::AcadosParameters() {
     for (double& v : all_parameters) v = 0.;
 }
 
-void AcadosParameters::printParameters(const mpcg::YamlNode& parameter_map) const {
+void AcadosParameters::printParameters(const YamlNode& parameter_map) const {
     for (int k = 0; k < SOLVER_N; ++k) {
         std::cout << "--- stage " << k << " ---\n";
         for (auto it = parameter_map.begin(); it != parameter_map.end(); ++it) {
@@ -149,9 +149,9 @@ void Solver::AcadosOutput::print() const {
 
 // ------------------------------------------------------------------- Solver
 Solver::Solver(int solver_id) : _solver_id(solver_id) {
-    _config = mpcg::yaml_load_file(SolverConfig::solverFile("solver_settings"));
-    _parameter_map = mpcg::yaml_load_file(SolverConfig::solverFile("parameter_map"));
-    _model_map = mpcg::yaml_load_file(SolverConfig::solverFile("model_map"));
+    _config = load_yaml_file(SolverConfig::solverFile("solver_settings"));
+    _parameter_map = load_yaml_file(SolverConfig::solverFile("parameter_map"));
+    _model_map = load_yaml_file(SolverConfig::solverFile("model_map"));
 
     N = _config["N"].as<int>();
     nu = _config["nu"].as<unsigned int>();
@@ -165,7 +165,7 @@ Solver::Solver(int solver_id) : _solver_id(solver_id) {
         fatal("the MI355X backend implements the contouring unicycle model (nx 5, or 6 with the slack state) and "
               "the curvature-aware bicycle (nx 6, nu 3)");
 
-    const mpcg::YamlNode& cfg = SolverConfig::settings();
+    const YamlNode& cfg = SolverConfig::settings();
     dt = cfg["integrator_step"].as<double>();
     _num_iterations = cfg["solver_settings"]["acados"]["iterations"].as<int>();
     const std::string solver_type = cfg["solver_settings"]["acados"]["solver_type"].as<std::string>();
@@ -308,7 +308,7 @@ int Solver::completeOneIteration() {
 }
 
 int Solver::model_index(const std::string& name) const {
-    const mpcg::YamlNode& e = _model_map[name];
+    const YamlNode& e = _model_map[name];
     if (!e.IsDefined()) throw std::runtime_error("Solver: no variable '" + name + "' in model_map.yaml");
     return e[1].as<int>();
 }

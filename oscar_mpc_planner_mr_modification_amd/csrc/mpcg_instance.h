@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 
 #include "mpcg.h"
@@ -19,11 +20,10 @@
 extern "C" {
 /* launcher of one compiled instance: enqueues the solve of `batch` problems on `stream`
  * and returns the hipError_t of the launch.  `workspace`: device memory on the stream's device
- * of at least MPCG_QUEUE_BYTES + batch x the instance's workspace bytes per solve (instances
- * whose stage blocks do not fit the LDS budget keep them there), whose first MPCG_QUEUE_BYTES
- * are zero before the first launch on it (the work queue of sqp_kernel, which every launch
- * leaves zeroed); or NULL for an instance without stage-block workspace (then one workgroup
- * per problem, no queue) */
+ * of at least MPCG_QUEUE_BYTES + batch x the instance's workspace bytes per solve: the work
+ * queue of sqp_kernel (zeroed on the stream before every launch), then per solve the stage
+ * blocks of the instances whose blocks do not fit the LDS budget and the interior point's
+ * iterative-refinement scratch */
 typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream,
                                     unsigned long long* stamps, void* workspace);
 /* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher, the
@@ -37,24 +37,36 @@ int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, i
 
 namespace mpcg {
 
-// grid of a work-queue launch: the workgroups the device holds at once (occupancy x CUs),
-// at most one per problem.  MPCG_QUEUE_GRID_PER_CU (A/B only) sets the workgroups per CU.
+// grid of a work-queue launch: the workgroups the stream's device holds at once (occupancy x
+// CUs), at most one per problem; cached per device.  MPCG_QUEUE_GRID_PER_CU (A/B only) sets the
+// workgroups per CU.
 template <class C, bool FULL>
-int queue_grid(int batch) {
-    static const int resident = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            return 0;
+int queue_grid(int batch, hipStream_t stream) {
+    constexpr int MAXDEV = 64;
+    static std::atomic<int> resident[MAXDEV];  // 0: not yet asked, -1: no answer
+    int dev = 0;
+    if ((stream ? hipStreamGetDevice(stream, &dev) : hipGetDevice(&dev)) != hipSuccess || dev < 0 || dev >= MAXDEV)
+        return batch;
+    int r = resident[dev].load(std::memory_order_relaxed);
+    if (r == 0) {
+        int cus = 0, per_cu = 0;
+        r = -1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
 #ifdef MPCG_QUEUE_GRID_PER_CU
-        per_cu = MPCG_QUEUE_GRID_PER_CU;
+            per_cu = MPCG_QUEUE_GRID_PER_CU;
 #else
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL>, 64, 0) != hipSuccess) return 0;
+            int cur = 0;
+            const bool sw = hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL>, 64, 0) != hipSuccess)
+                per_cu = 0;
+            if (sw) (void)hipSetDevice(cur);
 #endif
-        return per_cu > 0 ? per_cu * cus : 0;
-    }();
+            if (per_cu > 0) r = per_cu * cus;
+        }
+        resident[dev].store(r, std::memory_order_relaxed);
+    }
     // (no occupancy answer: one workgroup per problem, still through the queue)
-    return resident > 0 && resident < batch ? resident : batch;
+    return r > 0 && r < batch ? r : batch;
 }
 
 template <class C>
@@ -63,15 +75,19 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
     // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
     // the full variant only when the call needs QP memory, the warm start, the residuals or
     // the full SQP
-    if (gfh_doubles<C>() > 0 && !workspace) return (int)hipErrorInvalidValue;
+    if (ws_doubles<C>() > 0 && !workspace) return (int)hipErrorInvalidValue;
     unsigned* queue = C::QUEUE ? (unsigned*)workspace : nullptr;
     double* gws = workspace ? (double*)((char*)workspace + MPCG_QUEUE_BYTES) : nullptr;
+    const hipStream_t st = (hipStream_t)stream;
+    // the queue counter starts at zero for every launch, whatever an earlier launch on this
+    // workspace left behind (one that died mid-way included): a 256-byte memset on the stream
+    if (queue && hipMemsetAsync(queue, 0, MPCG_QUEUE_BYTES, st) != hipSuccess) return (int)hipGetLastError();
     if (io->stats || io->qp_in || io->qp_out || needs_full(*pr))
-        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(queue ? queue_grid<C, true>(batch) : batch), dim3(64), 0,
-                           (hipStream_t)stream, *pr, batch, *io, stamps, gws, queue);
+        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(queue ? queue_grid<C, true>(batch, st) : batch), dim3(64), 0,
+                           st, *pr, batch, *io, stamps, gws, queue);
     else
-        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(queue ? queue_grid<C, false>(batch) : batch), dim3(64), 0,
-                           (hipStream_t)stream, *pr, batch, *io, stamps, gws, queue);
+        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(queue ? queue_grid<C, false>(batch, st) : batch), dim3(64),
+                           0, st, *pr, batch, *io, stamps, gws, queue);
     return (int)hipGetLastError();
 }
 
@@ -92,7 +108,7 @@ const char* instance_traits() {
 template <class C>
 int register_instance() {
     return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM,
-                                  (long long)(gfh_doubles<C>() * sizeof(double)), instance_traits<C>());
+                                  (long long)(ws_doubles<C>() * sizeof(double)), instance_traits<C>());
 }
 
 }  // namespace mpcg

@@ -257,6 +257,21 @@ extern "C" {
 
 int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
 
+/* tests only (tests/test_queue.py): write `value` into the work-queue counter of the workspace that
+ * mpcg_solve keeps for `stream`, as a launch that died mid-way would leave it.  Returns 0, or -1
+ * when the stream has no workspace yet. */
+int mpcg_debug_set_queue(void* stream, unsigned value) {
+    std::lock_guard<std::mutex> l(mpcg::g_ws_mutex);
+    for (const mpcg::StreamWs& w : mpcg::g_ws)
+        if (w.stream == stream && w.ptr) {
+            static unsigned v;
+            v = value;
+            if (hipMemcpyAsync(w.ptr, &v, sizeof v, hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess) return -1;
+            return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? 0 : -1;
+        }
+    return -1;
+}
+
 /* diagnostic builds only: device buffer of batch x 20 u64 phase-cycle sums */
 void mpcg_debug_set_stamp_buffer(unsigned long long* dev_ptr) { mpcg::g_stamps = dev_ptr; }
 
@@ -379,8 +394,6 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->qp_tol = 1e-5;
     pr->qp_iter_max = 50;
     pr->reg_eps = 1e-4;
-    pr->qp_mu0 = 1.0;
-    pr->qp_thr0 = 1.0;
     pr->res_eq_fail = 1e-2;
     // QP start as the reference configures it: qp_solver_warm_start = 2 (generate_acados_solver.py:173)
     // with acados' warm_start_first_qp off, so the first QP of each acados call starts cold -- every
@@ -393,9 +406,31 @@ int mpcg_problem_from_map_model(mpcg_problem* pr, int model, int N, int nx, int 
     pr->nlp_solver = MPCG_NLP_SQP_RTI;
     pr->nlp_max_iter = 100;
     pr->nlp_tol = 1e-2;
-    // the interior point's t / lambda floor
-    pr->qp_t_min = 1e-12;
-    pr->qp_mu_max = 1e8;
+    // the interior point as acados configures HPIPM
+    mpcg_problem_set_qp_profile(pr, MPCG_QP_HPIPM);
+    return 0;
+}
+
+int mpcg_problem_set_qp_profile(mpcg_problem* pr, int profile) {
+    if (!pr || (profile != MPCG_QP_HPIPM && profile != MPCG_QP_ROBUST)) {
+        mpcg::g_err = "unknown QP profile";
+        return -1;
+    }
+    const bool h = profile == MPCG_QP_HPIPM;
+    pr->qp_profile = profile;
+    // HPIPM BALANCE (d_ocp_qp_ipm_arg_set_default, applied by acados before the reference's qp_tol /
+    // qp_solver_iter_max / qp_solver_warm_start): mu0 1e1, init_var's thr0 1e-1 with the primal box
+    // move, t_min = lam_min 1e-16, cond_pred_corr 1, itref_corr_max 2, sigma (mu_aff / mu)^3, the
+    // iteration cap before convergence, no divergence test.  Robust: the round-4 constants
+    pr->qp_mu0 = h ? 10.0 : 1.0;
+    pr->qp_thr0 = h ? 0.1 : 1.0;
+    pr->qp_t_min = h ? 1e-16 : 1e-12;
+    pr->qp_mu_max = h ? 0.0 : 1e8;
+    pr->qp_init_move = h;
+    pr->qp_cond_pred_corr = h;
+    pr->qp_itref_corr_max = h ? 2 : 0;
+    pr->qp_sigma_clip = !h;
+    pr->qp_maxit_first = h;
     return 0;
 }
 

@@ -365,6 +365,18 @@ template <class C>
 __host__ __device__ constexpr size_t gfh_doubles() {
     return lds_gfh<C>() ? (size_t)C::N * C::NFR * C::NFC + (size_t)(C::N + 1) * C::NHP : 0;
 }
+// doubles of one solve's iterative-refinement scratch (qp_itref_corr_max, the rare path: the
+// unrefined direction's step [N+1][NZ] and dynamics multipliers [N][NX], and the refinement's
+// dynamics right-hand side [N][NX])
+template <class C>
+__host__ __device__ constexpr size_t itref_doubles() {
+    return (size_t)(C::N + 1) * C::NZ + 2 * (size_t)C::N * C::NX;
+}
+// one solve's global workspace: the GFH blocks, then the refinement scratch
+template <class C>
+__host__ __device__ constexpr size_t ws_doubles() {
+    return gfh_doubles<C>() + itref_doubles<C>();
+}
 
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
 // production build compiles them out).  Read shares, not absolute times.
@@ -667,8 +679,8 @@ __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io
 // frees, so with a grid of one workgroup per solve each XCD works through a fixed eighth of the
 // batch and every solve pays a workgroup launch; here a wave that finishes early takes the next
 // solve of the whole batch (the tail).  Every wave leaves the loop on its first
-// ticket >= batch; the last workgroup out (queue[1] counts them) zeroes both words for the next
-// launch on the same workspace, which the stream orders after this one.
+// ticket >= batch.  launch_instance zeroes the queue words on the launch stream before every
+// launch, so no launch depends on how the previous one on the same workspace ended.
 template <class C, bool FULL = false>
 __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps,
@@ -696,10 +708,6 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
         for (int sol = q ? next() : (int)blockIdx.x; sol < batch; sol = q ? next() : batch) {
             sqp_solve<C, FULL>(pr, batch, io, stamps, gws, sol);
             wave_sync();
-        }
-        if (q && threadIdx.x == 0 && atomicAdd(&queue[1], 1u) == gridDim.x - 1) {
-            atomicExch(&queue[0], 0u);
-            atomicExch(&queue[1], 0u);
         }
     }
 }

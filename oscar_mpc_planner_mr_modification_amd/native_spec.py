@@ -41,6 +41,9 @@ class MpcgProblem(C.Structure):
         ("nlp_solver", C.c_int), ("nlp_max_iter", C.c_int), ("nlp_tol", C.c_double), ("qp_warm_first", C.c_int),
         # ABI 7
         ("qp_t_min", C.c_double), ("qp_mu_max", C.c_double),
+        # ABI 8: the interior point's profile
+        ("qp_profile", C.c_int), ("qp_init_move", C.c_int), ("qp_cond_pred_corr", C.c_int),
+        ("qp_itref_corr_max", C.c_int), ("qp_sigma_clip", C.c_int), ("qp_maxit_first", C.c_int),
     ]
 
 
@@ -48,9 +51,21 @@ class MpcgProblem(C.Structure):
 # epsilon, tol) + the IPM's cold start; qp_warm_start=2 (the reference's qp_solver_warm_start, :173)
 # with acados' warm_start_first_qp off (qp_warm_first=0) starts every SQP-RTI QP cold and the
 # later QPs of a full SQP call (solver_type="SQP") warm (DESIGN.md §2 "QP start")
-DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, qp_mu0=1.0, qp_thr0=1.0, res_eq_fail=1e-2,
+DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, res_eq_fail=1e-2,
                        qp_warm_start=2, qp_ws_thr=0.1, qp_warm_first=0, solver_type="SQP_RTI", nlp_max_iter=100,
-                       nlp_tol=1e-2, qp_t_min=1e-12, qp_mu_max=1e8)
+                       nlp_tol=1e-2, qp_profile="hpipm")
+# The interior point's profiles (mpcg_problem_set_qp_profile in libmpcg.so writes the
+# same values): "hpipm", the default, restates HPIPM's BALANCE mode as acados configures it (the
+# reference sets four QP options and leaves the rest at acados' defaults, generate_acados_solver.py:162-173);
+# "robust" is round 4's interior point.  Any field can be overridden by name.
+QP_PROFILES = {
+    "hpipm": dict(qp_profile_id=0, qp_mu0=10.0, qp_thr0=0.1, qp_t_min=1e-16, qp_mu_max=0.0, qp_init_move=1,
+                  qp_cond_pred_corr=1, qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1),
+    "robust": dict(qp_profile_id=1, qp_mu0=1.0, qp_thr0=1.0, qp_t_min=1e-12, qp_mu_max=1e8, qp_init_move=0,
+                   qp_cond_pred_corr=0, qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0),
+}
+QP_FIELDS = ("qp_mu0", "qp_thr0", "qp_t_min", "qp_mu_max", "qp_init_move", "qp_cond_pred_corr", "qp_itref_corr_max",
+             "qp_sigma_clip", "qp_maxit_first")
 NLP_SOLVER = {"SQP_RTI": 0, "SQP": 1}
 # ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
 UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
@@ -80,8 +95,6 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.qp_tol = o["qp_tol"]
     pr.qp_iter_max = o["qp_iter_max"]
     pr.reg_eps = o["reg_eps"]
-    pr.qp_mu0 = o["qp_mu0"]
-    pr.qp_thr0 = o["qp_thr0"]
     pr.res_eq_fail = o["res_eq_fail"]
     pr.qp_warm_start = o["qp_warm_start"]
     pr.qp_ws_thr = o["qp_ws_thr"]
@@ -89,8 +102,10 @@ def problem_from_layout(layout: Layout, **opts) -> MpcgProblem:
     pr.nlp_solver = NLP_SOLVER[o["solver_type"]]
     pr.nlp_max_iter = o["nlp_max_iter"]
     pr.nlp_tol = o["nlp_tol"]
-    pr.qp_t_min = o["qp_t_min"]
-    pr.qp_mu_max = o["qp_mu_max"]
+    prof = QP_PROFILES[o["qp_profile"]]
+    pr.qp_profile = prof["qp_profile_id"]
+    for f in QP_FIELDS:
+        setattr(pr, f, o.get(f, prof[f]))
     return pr
 
 
@@ -137,12 +152,12 @@ class MpcgScenarioIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size", "mpcg_qp_mem_size",
            "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",
            "mpcg_prepare_scenario", "mpcg_select_lowest_cost_device", "mpcg_winner_records_device",
            "mpcg_release_stream_workspace",
-           "mpcg_instance_traits")
+           "mpcg_instance_traits", "mpcg_problem_set_qp_profile")
 
 

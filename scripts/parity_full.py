@@ -38,7 +38,35 @@ def inputs(cfg, S, first=0):
     return lay, b
 
 
-def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQP_RTI"):
+def perturbed_outcomes(lay, b, idx, opts, K=16, seed=1):
+    """Rounding-sensitivity by evidence, kernel-agnostic: the default oracle build on K copies of
+    solve i whose warm start moved by at most one ulp per entry (copy 0 unperturbed).  Returns per
+    solve the exit codes of the K runs and their trajectories' largest distance to the unperturbed
+    run's: a solve whose exit code or successful trajectory (beyond 1e-4) changes under a one-ulp
+    change of its inputs is decided by rounding."""
+    import oracle_py
+    out = {}
+    if len(idx) == 0:
+        return out
+    rng = np.random.default_rng(seed)
+    P = np.repeat(b.params[idx], K, 0)
+    W = np.repeat(b.warm[idx], K, 0).copy()
+    X = np.repeat(b.xinit[idx], K, 0)
+    st = rng.integers(-1, 2, size=W.shape)
+    st[::K] = 0
+    W = np.where(st > 0, np.nextafter(W, np.inf), np.where(st < 0, np.nextafter(W, -np.inf), W))
+    r = oracle_py.Oracle(lay, **opts).solve_batch(P, W, X, nthreads=16)
+    for n, i in enumerate(idx):
+        sl = slice(n * K, (n + 1) * K)
+        ex = r["status"][sl]
+        xt = r["xtraj"][sl]
+        d = np.abs(xt - xt[0]).reshape(K, -1).max(1)
+        out[int(i)] = {"exits": ex.tolist(), "dx": d, "xtraj": xt,
+                       "sensitive": bool((ex != ex[0]).any() or ((ex == 1) & (ex[0] == 1) & (d > 1e-4)).any())}
+    return out
+
+
+def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQP_RTI", qp_profile="hpipm"):
     """GPU vs oracle on the bench batch; ws / warm_first: qp_solver_warm_start and
     warm_start_first_qp (default: warm-start the first QP too when ws == 2, the restated
     warm start; ws 2 with warm_first 0 is the reference's configuration, cold in SQP-RTI);
@@ -62,7 +90,7 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     lay, b = inputs(cfg, S, first)
     dev = torch.device("cuda:0")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    opts = dict(qp_warm_start=ws, qp_warm_first=warm_first, solver_type=solver_type)
+    opts = dict(qp_warm_start=ws, qp_warm_first=warm_first, solver_type=solver_type, qp_profile=qp_profile)
     pr = native.problem_from_layout(lay, **opts)
     P, W, X = t(b.params), t(b.warm), t(b.xinit)
     out = native.solve_batch_device(pr, P, W, X)
@@ -118,6 +146,23 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     same_k = got["exit"] == kf["status"]
     # successful solves more than 1e-4 apart although no QP of either side stopped at the cap
     over_capfree = ok & (dx > 1e-4) & capfree
+    # every solve on which the GPU parts from the default build (exit, or successful trajectories
+    # more than 1e-4 apart): is the default build's own result decided by rounding?  Evidence: the
+    # two kernel-agnostic builds part on it (above), or a one-ulp perturbation of its warm start
+    # changes it (perturbed_outcomes); on such a solve the GPU must end like one of the oracle runs
+    # (an exit code some build or perturbed run produced, and, if successful, a trajectory within
+    # 1e-4 of one of theirs), everywhere else it is held to the default build at the north_star bar
+    parted = ~same | (ok & (dx > 1e-4))
+    cand = np.flatnonzero(parted)
+    pert = perturbed_outcomes(lay, b, cand, opts)
+    sens = np.zeros(len(same), bool)
+    like_run = np.zeros(len(same), bool)
+    for i, po in pert.items():
+        sens[i] = po["sensitive"]
+        # (a rounding-decided trajectory is not held to 1e-4: each one-ulp run ends elsewhere)
+        like_run[i] = int(got["exit"][i]) in set(po["exits"]) | {int(ref["status"][i]), int(lit["status"][i])}
+    rdec = decided | sens
+    unexplained = parted & ~rdec
     return {"config": cfg, "qp_warm_start": ws, "qp_warm_first": warm_first, "solver_type": solver_type,
             "oracle": "literal" if literal else "default (HPIPM forms)", "gpu_variant": variant, **lean_full,
             "kernel_forms_exit_agreement": float(same_k.mean()),
@@ -141,6 +186,10 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
             "maxiter_info_agreement": float((got["info"][:, 3] == ref["qp_maxiter"]).mean()),
             "same_path_failed_dx": float(dx[path].max()) if path.any() else None,
             "stats_max_rel_diff": float(st_rel),
+            "stats_worst": ({"i": int(iw), "gpu": got["stats"][iw].tolist(), "oracle": st[iw].tolist(),
+                             "gpu_info": got["info"][iw].tolist(), "exit": int(got["exit"][iw])}
+                            if (same & capfree).any() and (iw := int(np.flatnonzero(same & capfree)[
+                                np.argmax(st_relv[same & capfree])])) >= 0 else None),
             "disagreeing": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
                              "gpu_info": got["info"][i].tolist(), "oracle_sqp": int(ref["sqp_iter"][i]),
                              "oracle_qp_status": int(ref["qp_status"][i])} for i in dis[:20]],
@@ -160,7 +209,23 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
             "capfree_exit_agreement": float(same[capfree].mean()) if capfree.any() else None,
             "capfree_max_abs_dx_success": float(dx[capfree & ok].max()) if (capfree & ok).any() else None,
             "n_success_dx_over_1e-4_capfree": int(over_capfree.sum()),
-            "n_success_dx_over_1e-4_capped": int((ok & (dx > 1e-4) & ~capfree).sum())}
+            "n_success_dx_over_1e-4_capped": int((ok & (dx > 1e-4) & ~capfree).sum()),
+            "qp_profile": qp_profile,
+            "n_parted": int(parted.sum()),
+            "n_rounding_decided_perturbation": int((sens & ~decided).sum()),
+            "parted_rounding_decided": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
+                                         "perturbed_exits": sorted(set(pert[int(i)]["exits"])),
+                                         "perturbed_max_dx": float(pert[int(i)]["dx"].max()),
+                                         "gpu_dx_default": float(dx[i]), "builds_part": bool(decided[i]),
+                                         "gpu_ends_like_a_run": bool(like_run[i])}
+                                        for i in np.flatnonzero(parted & rdec)[:40]],
+            "n_parted_rounding_decided": int((parted & rdec).sum()),
+            "parted_rounding_decided_end_like_a_run": bool(like_run[parted & rdec].all()),
+            "n_unexplained": int(unexplained.sum()),
+            "unexplained": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
+                             "gpu_info": got["info"][i].tolist(), "oracle_qp_iter": int(ref["qp_iter"][i]),
+                             "gpu_dx_default": float(dx[i])} for i in np.flatnonzero(unexplained)[:20]],
+            "n_rounding_decided_any": int(rdec.sum())}
 
 
 def main():
@@ -171,11 +236,12 @@ def main():
     ap.add_argument("--warm-first", type=int, default=None)
     ap.add_argument("--literal", action="store_true", help="against the literal-forms oracle build")
     ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"))
+    ap.add_argument("--qp-profile", default="hpipm", choices=("hpipm", "robust"))
     args = ap.parse_args()
     for cfg in args.configs.split(","):
         for ws in (int(w) for w in args.ws.split(",")):
             r = compare(cfg, args.scenes or DEFAULT_SCENES[cfg], ws, warm_first=args.warm_first, literal=args.literal,
-                        solver_type=args.solver_type)
+                        solver_type=args.solver_type, qp_profile=args.qp_profile)
             print(json.dumps(r), flush=True)
 
 

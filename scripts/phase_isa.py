@@ -22,6 +22,7 @@ CFG = {"C1": "20ELi4ELi4ELi0ELi5ELi0", "C2": "20ELi8ELi8ELi0ELi5ELi0", "C4": "30
        "JS": "30ELi4ELi4ELi0ELi5ELi0", "JD": "30ELi5ELi5ELi0ELi5ELi0", "C5": "20ELi0ELi0ELi24ELi6ELi0",
        "C3": "30ELi0ELi0ELi12ELi6ELi1"}
 # mpcg_sqp.h STAMP_END indices
+EXTRA = os.environ.get("PHASE_ISA_FLAGS", "").split()
 PHASES = {0: "linearisation", 1: "QP start", 2: "residuals (+ predictor barrier terms)", 3: "barrier terms + Newton gradient",
           4: "Riccati factorisation", 5: "vector chains + feedback", 7: "row steps, step length", 8: "iterate update"}
 
@@ -55,7 +56,7 @@ def main():
     fam = FAMILY[args.config]
     asm = f"/tmp/phase_isa_{fam}.s"
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{os.path.join(ROOT, 'include')}",
-                    f"-I{CSRC}", "-DMPCG_MARKERS", "--cuda-device-only", "-S", os.path.join(CSRC, f"mpcg_inst_{fam}.hip"),
+                    f"-I{CSRC}", "-DMPCG_MARKERS", *EXTRA, "--cuda-device-only", "-S", os.path.join(CSRC, f"mpcg_inst_{fam}.hip"),
                     "-o", asm], check=True, stderr=subprocess.DEVNULL)
     lines = open(asm).read().split("\n")
     name = f"_ZN4mpcg10sqp_kernelINS_3CfgILi{CFG[args.config]}EEELb0E"
@@ -111,7 +112,7 @@ def main():
         tot_f += fl
         rows.append((p, ips, fl))
         print(f"  {p} {PHASES.get(p, '?'):38s} {a['regions']:6d} {a['n']:7d} {a['f64']:6d} {a['valu']:6d} {a['lds']:5d} "
-              f"{a['salu']:5d} {a['mem'] + a['scratch']:7d} {ips:12.0f} {ips / tot_i:6.1%} {fl:21.3e}")
+              f"{a['salu']:5d} {a['mem']:4d}+{a['scratch']:<4d} {ips:12.0f} {ips / tot_i:6.1%} {fl:21.3e}")
     lin = flopmodel.linearisation_ops(lay) * S
     parts = {k: v * Q for k, v in flopmodel.ipm_iteration_ops_by_part(lay).items()}
     ipm = sum(parts.values())

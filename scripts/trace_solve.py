@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--warm-first", type=int, default=0)
     ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"))
     ap.add_argument("--variant", default="lean", choices=("lean", "full"))
+    ap.add_argument("--qp-profile", default="robust", choices=("hpipm", "robust"),
+                    help="the interior point's profile (DESIGN.md §2.2) of both sides")
     ap.add_argument("--forms", default="hpipm", choices=("hpipm", "literal", "kernel"),
                     help="the oracle build to trace (oracle/mpcg_oracle.c \"Arithmetic forms\")")
     args = ap.parse_args()
@@ -75,7 +77,8 @@ def main():
     import tempfile
     inp = os.path.join(tempfile.gettempdir(), f"mpcg_trace_inputs_{os.getpid()}.npz")
     np.savez(inp, params=b.params, warm=b.warm, xinit=b.xinit)
-    opts = dict(qp_warm_start=args.ws, qp_warm_first=args.warm_first, solver_type=args.solver_type)
+    opts = dict(qp_warm_start=args.ws, qp_warm_first=args.warm_first, solver_type=args.solver_type,
+                qp_profile=args.qp_profile)
     # the GPU side in a child process (the trace library replaces libmpcg.so there)
     code = (f"import sys, numpy as np, torch; sys.path[:0]={[ROOT]!r}; "
             "from oscar_mpc_planner_mr_modification_amd import native; "

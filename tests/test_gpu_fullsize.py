@@ -3,23 +3,26 @@ C2 1024 scenes x 8 guesses, C4 2048 x 8 (one GPU's shard of 16384), C5 2048 x 4
 parallel scenario solvers started from the previous plan and (C5B) from the braking
 plan, C3 4096 bicycle solves, JS (the shipped jackalsimulator solver) 4096 x 5, JD (the
 shipped jackal / dingo solver, N 30 with 5 obstacles) 4096 x 5, C1 1024 scenes; the
-reference's QP start (qp_solver_warm_start 2, warm_start_first_qp off).
+reference's QP start (qp_solver_warm_start 2, warm_start_first_qp off) and the interior point
+as acados configures HPIPM (the default QP profile), plus the robust profile
+on C2 and C5B.
 
 The product launch -- the lean kernel variant that bench.py and mpcg_solve_batch_device run
 -- is compared with the oracle's default build (HPIPM's arithmetic forms) on every solve:
-identical exit codes and, for successful solves, trajectories within 1e-4 (north_star) --
-except where a QP of the solve stopped at the 50-iteration cap on both sides: the RTI loop
-then ends on that QP's unconverged step, which is wherever the stalled interior point stood
-(DESIGN.md §2 "QP start"), so only the exit code is held there (C5B: 1 of 8,192 copies).  The
-FULL kernel variant (stats buffer: the NLP residuals of the drop-in's AcadosInfo) must end
-every solve like the lean one.  The literal-forms oracle build tells which solves rounding
-decides; with the interior point's t / lambda floor no bench batch has one.
+identical exit codes and, for successful solves, trajectories within 1e-4 (north_star).  The
+only exemption is a solve whose oracle result is itself decided by rounding, by evidence
+that uses the oracle alone: the two kernel-agnostic builds (HPIPM's forms, the literal forms)
+part on it, or a one-ulp perturbation of its warm start changes its exit code or moves its
+successful trajectory by more than 1e-4 (scripts/parity_full.py perturbed_outcomes).  On
+such a solve the GPU must end with an exit code one of those oracle runs produced.  No
+other exemption: no cap-based allowance (the C5B copy 299 record).
+
+The FULL kernel variant (stats buffer: the NLP residuals of the drop-in's AcadosInfo) must end
+every solve like the lean one.
 
 solver_type SQP (one full acados SQP call per solve, the FULL variant): C2 and C4 at bench
-size, with the same bar on every solve whose QPs all converged on both sides; a solve in
-which some QP stopped at the 50-iteration cap applies that QP's unconverged step and carries
-it into the next, warm-started QP, so its path is set by where the stalled interior point
-stood (DESIGN.md §2 "QP start").  Those solves must still end with the same exit code."""
+size, with the same bar, and the NLP residuals of every solve whose QPs all converged on both
+sides against the oracle's."""
 import os
 import sys
 
@@ -30,27 +33,30 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _assert_parity(r):
+    # every solve on which the GPU parts from the default build is rounding-decided by evidence
+    assert r["n_unexplained"] == 0, r["unexplained"]
+    assert r["parted_rounding_decided_end_like_a_run"], r["parted_rounding_decided"]
+    # ... and such solves stay rare
+    assert r["n_parted_rounding_decided"] <= 0.005 * r["solves"], r["parted_rounding_decided"]
+
+
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg", ["C2", "C4", "C5", "C5B", "C3", "JS", "JD", "C1"])
-def test_fullsize_parity(cfg):
+@pytest.mark.parametrize("cfg,profile", [(c, "hpipm") for c in ("C2", "C4", "C5", "C5B", "C3", "JS", "JD", "C1")] +
+                         [("C2", "robust"), ("C5B", "robust")])
+def test_fullsize_parity(cfg, profile):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from parity_full import DEFAULT_SCENES, compare
 
-    r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0)
-    print({k: v for k, v in r.items() if k != "rounding_decided"})
+    r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0, qp_profile=profile)
+    print({k: v for k, v in r.items() if k not in ("rounding_decided", "parted_rounding_decided")})
     # the kernel the bench times
     assert r["gpu_variant"] == "lean"
-    # no rounding-decided solve: the default build decides every exit and every trajectory
-    assert r["n_rounding_decided"] == 0, r["rounding_decided"]
-    assert r["exit_agreement"] == 1.0, r["disagreeing"]
-    assert r["n_success_dx_over_1e-4_capfree"] == 0, r["success_dx_over_1e-4"]
-    assert r["capfree_max_abs_dx_success"] <= 1e-4
-    assert r["n_success_dx_over_1e-4_capped"] <= 0.001 * r["solves"], r["success_dx_over_1e-4"]
-    assert r["same_path_failed_dx"] is None or r["same_path_failed_dx"] <= 1e-4
+    _assert_parity(r)
     # the FULL variant ends every solve like the lean one
     assert r["lean_full_exit_equal"] and r["lean_full_info_equal"], r
     assert r["lean_full_max_abs_dx"] <= 1e-9, r["lean_full_max_abs_dx"]
-    # the NLP residuals of the FULL variant against the oracle's
+    # the NLP residuals of the FULL variant against the oracle's (solves whose QPs all converged)
     assert r["stats_max_rel_diff"] <= 1e-6, r["stats_max_rel_diff"]
     floor = {"C5": 0.85, "C5B": 0.7}.get(cfg, 0.9)
     assert r["success_frac"] >= floor, r["success_frac"]
@@ -65,10 +71,15 @@ def test_fullsize_parity_full_sqp(cfg):
     from parity_full import DEFAULT_SCENES, compare
 
     r = compare(cfg, DEFAULT_SCENES[cfg], 2, warm_first=0, solver_type="SQP")
-    print({k: v for k, v in r.items() if k != "rounding_decided"})
+    print({k: v for k, v in r.items() if k not in ("rounding_decided", "parted_rounding_decided")})
     assert r["gpu_variant"] == "full"
-    assert r["n_rounding_decided"] == 0, r["rounding_decided"]
-    assert r["exit_agreement"] == 1.0, r["disagreeing"]
-    assert r["n_success_dx_over_1e-4_capfree"] == 0, r["success_dx_over_1e-4"]
-    assert r["capfree_max_abs_dx_success"] <= 1e-4
+    _assert_parity(r)
+    # the NLP residuals the drop-in's AcadosInfo reports, on the solves whose QPs all converged
+    assert r["stats_max_rel_diff"] <= SQP_STATS_TOL, r["stats_max_rel_diff"]
     assert r["capfree_frac"] >= 0.95
+
+
+# full SQP: the final NLP residuals are read at the last linearisation point, whose multipliers are
+# the last QP's; two trajectories 1e-5 apart can carry residuals that differ in the 1e-3 range
+# relative to max(1, |residual|)
+SQP_STATS_TOL = 1e-2

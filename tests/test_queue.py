@@ -1,7 +1,7 @@
 """The work-queue launch of the N <= 20 instances (mpcg_sqp.h sqp_kernel, mpcg_instance.h
 queue_grid; DESIGN.md §3.7 "The work queue"): a resident grid takes solves from an atomic
-counter at the head of the per-stream workspace, and every launch leaves that counter zeroed
-for the next one.  Consecutive launches of different sizes on one stream -- more solves than
+counter at the head of the per-stream workspace, which launch_instance zeroes on the stream before
+every launch.  Consecutive launches of different sizes on one stream -- more solves than
 resident workgroups, fewer than resident workgroups, the FULL variant in between -- must give
 every solve the same result, bit for bit, as one launch of the whole batch: a counter left
 non-zero would skip solves (their outputs stay at the fill value), and a solve that depended on
@@ -51,3 +51,37 @@ def test_queue_launches_of_any_size_agree(cfg, n_scenes):
         assert np.array_equal(again[k], ref[k], equal_nan=True), (cfg, k, "repeat launch")
         # the FULL variant (stats buffer) ends every solve like the lean one (tests/test_gpu_fullsize.py)
         assert np.array_equal(full_variant[k], ref[k], equal_nan=True), (cfg, k, "FULL variant")
+
+
+@pytest.mark.timeout(300)
+def test_queue_starts_clean_after_a_dirty_counter():
+    """a counter left non-zero (as a launch that died mid-way would leave it) must not make the next
+    launch skip solves: every solve is written and equals the clean launch bit for bit"""
+    import ctypes as C
+
+    import torch
+
+    from oscar_mpc_planner_mr_modification_amd import native
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
+    from oscar_mpc_planner_mr_modification_amd.synthetic import make_batch
+
+    assert torch.cuda.is_available(), "gpu test on a box without a GPU"
+    dev = torch.device("cuda:0")
+    lay = config_layout("C2")
+    b = make_batch(lay, 140, 8, seed=11)
+    pr = native.problem_from_layout(lay)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    P, W, X = t(b.params), t(b.warm), t(b.xinit)
+    s = torch.cuda.current_stream(dev)
+    ref = native.solve_batch_device(pr, P, W, X, stream=s)
+    torch.cuda.synchronize()
+    ref = {k: v.cpu().numpy() for k, v in ref.items()}
+    lib = native.lib
+    lib.mpcg_debug_set_queue.restype = C.c_int
+    for dirty in (37, 1100, 0xFFFFFFF0):
+        assert lib.mpcg_debug_set_queue(C.c_void_p(s.cuda_stream), C.c_uint(dirty)) == 0
+        out = {k: torch.full_like(torch.from_numpy(v).to(dev), -7) for k, v in ref.items()}
+        native.solve_batch_device(pr, P, W, X, out=out, stream=s)
+        torch.cuda.synchronize()
+        for k in ("xtraj", "utraj", "pobj", "exit", "info"):
+            assert np.array_equal(out[k].cpu().numpy(), ref[k], equal_nan=True), (dirty, k)

@@ -1,5 +1,6 @@
 """Rounding-sensitivity record of the C5 SH-MPC QPs and the t / lambda floor that settles it
-(DESIGN.md §2.2, §3.2), CPU only.
+(DESIGN.md §2.2, §3.2), CPU only.  The record is of the robust QP profile (round 4's interior
+point, qp_profile="robust"), whose floor was chosen on it.
 
 Copy 7799 of the C5 bench batch (scene 1949, parallel solver 3) reaches, in its fifth QP, the
 dual-degenerate drift of the pinned slack rows: the multipliers of the slack's lower bound grow
@@ -32,8 +33,8 @@ def _path(r, i):
 
 def test_without_the_floor_the_builds_part_on_the_dual_degenerate_copy(oracle_mod, scene1949):
     lay, b = scene1949
-    a = oracle_mod.Oracle(lay, qp_t_min=0.0).solve_batch(b.params, b.warm, b.xinit)
-    c = oracle_mod.Oracle(lay, literal=True, qp_t_min=0.0).solve_batch(b.params, b.warm, b.xinit)
+    a = oracle_mod.Oracle(lay, qp_profile="robust", qp_t_min=0.0).solve_batch(b.params, b.warm, b.xinit)
+    c = oracle_mod.Oracle(lay, literal=True, qp_profile="robust", qp_t_min=0.0).solve_batch(b.params, b.warm, b.xinit)
     dx = np.abs(a["xtraj"] - c["xtraj"]).reshape(4, -1).max(1)
     # copies 0-2: the same result to rounding
     assert dx[:3].max() < 1e-12
@@ -45,7 +46,7 @@ def test_without_the_floor_the_builds_part_on_the_dual_degenerate_copy(oracle_mo
 
 def test_with_the_floor_every_build_takes_one_path(oracle_mod, scene1949):
     lay, b = scene1949
-    runs = [oracle_mod.Oracle(lay, forms=f).solve_batch(b.params, b.warm, b.xinit) for f in ("hpipm", "literal", "kernel")]
+    runs = [oracle_mod.Oracle(lay, forms=f, qp_profile="robust").solve_batch(b.params, b.warm, b.xinit) for f in ("hpipm", "literal", "kernel")]
     for r in runs[1:]:
         np.testing.assert_array_equal(r["status"], runs[0]["status"])
         np.testing.assert_array_equal(r["qp_iter"], runs[0]["qp_iter"])
