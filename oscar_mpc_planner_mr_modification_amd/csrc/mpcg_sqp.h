@@ -148,8 +148,10 @@ struct Cfg {
     // (profiles/r03c_variant_storeit.jsonl).  C5 stored: 20.89 -> 20.68 ms.  Without it C5 is
     // scratch-free (28 B/lane with it) but slower, 20.69 -> 20.91 (profiles/r03k_ab.jsonl,
     // MPCG_STORE_IT_MAX=12).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
+// (round 5: 14 -> 13, C5 stops storing it: with the HPIPM profile's cold start and refinement
+// test its stored 1/t pushed the residual and step passes into scratch, 232 -> 80 B/lane)
 #ifndef MPCG_STORE_IT_MAX
-#define MPCG_STORE_IT_MAX 14
+#define MPCG_STORE_IT_MAX 13
 #endif
 #ifdef MPCG_STORE_IT_ANY
     static constexpr bool STORE_IT_PARTS_OK = true;

@@ -53,7 +53,9 @@ def main():
                 d = json.loads(line[-1])
                 print(json.dumps({"variant": name, "config": cfg, "rep": rep, "value": d["value"],
                                   "kernel_ms": d["roofline"]["kernel_ms"], "ms_per_step": d["ms_per_step"],
-                                  "qp_iters": d["solver_stats"]["qp_iters_per_solve"]}), flush=True)
+                                  "qp_iters": d["solver_stats"]["qp_iters_per_solve"],
+                                  "qp_profile": d["solver_stats"].get("qp_profile"),
+                                  "alt": d.get("qp_profile_alt")}), flush=True)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@ on the bench batches, with the oracle (test infrastructure):
 4. the interior point's divergence test qp_mu_max in full SQP (rounding-decided solves) and in
    SQP-RTI (what it changes against round 3's 1e16).
 
-    python scripts/ipm_constants.py > profiles/r04_ipm_constants.txt
+    python scripts/ipm_constants.py [parts: 1 2 3 4] > profiles/r04_ipm_constants.txt
 """
 import os
 import sys
@@ -26,6 +26,8 @@ NT = int(os.environ.get("OMP_NUM_THREADS", "8") or 8)
 
 
 def run(lay, b, forms="hpipm", **opts):
+    # these experiments chose the robust profile's constants (round 4)
+    opts.setdefault("qp_profile", "robust")
     return oracle_py.Oracle(lay, forms=forms, **opts).solve_batch(b.params, b.warm, b.xinit, nthreads=NT)
 
 
@@ -41,6 +43,18 @@ def summary(r):
 
 
 def main():
+    parts = set(sys.argv[1:]) or {"1", "2", "3", "4"}
+    if "1" in parts:
+        part1()
+    if "2" in parts:
+        part2()
+    if "3" in parts:
+        part3()
+    if "4" in parts:
+        part4()
+
+
+def part1():
     print("# 1. t / lambda floor vs rounding-decided SH-MPC copies (2048 scenes x 4 copies)")
     batches = {c: inputs(c, 2048) for c in ("C5", "C5B")}
     for tmin in (0.0, 1e-16, 1e-14, 1e-13, 1e-12, 1e-8):
@@ -50,6 +64,9 @@ def main():
             neither = parted(R["kernel"], R["hpipm"]) & parted(R["kernel"], R["literal"])
             print(f"{cfg} qp_t_min {tmin:g}: rounding-decided {int(dec.sum())} {np.flatnonzero(dec)[:12].tolist()} "
                   f"kernel-forms like neither {int(neither.sum())} | {summary(R['hpipm'])}", flush=True)
+
+
+def part2():
     print("\n# 2. the floor 1e-12 against no floor elsewhere (HPIPM-forms build)")
     for cfg, S in (("C2", 1024), ("C1", 1024), ("C4", 512), ("C3", 1024), ("JS", 1024), ("JD", 1024)):
         lay, b = inputs(cfg, S)
@@ -59,11 +76,17 @@ def main():
         dx = np.abs(a["xtraj"] - c["xtraj"]).reshape(len(same), -1)[ok].max() if ok.any() else 0.0
         print(f"{cfg} {len(same)} solves: exit agreement {same.mean():.6f} max |dx| {dx:.2e} "
               f"ipm/solve {a['qp_iter'].mean():.3f} -> {c['qp_iter'].mean():.3f}", flush=True)
+
+
+def part3():
     print("\n# 3. cold-start constants (t = max(gap, thr0), lambda = mu0 / t, dz = 0)")
     for cfg, S in (("C2", 512), ("C5", 1024), ("C4", 512), ("C3", 1024)):
         lay, b = inputs(cfg, S)
         for mu0, thr0 in ((1.0, 1.0), (1.0, 0.1), (10.0, 0.1), (10.0, 1.0)):
             print(f"{cfg} mu0 {mu0:g} thr0 {thr0:g}: {summary(run(lay, b, qp_mu0=mu0, qp_thr0=thr0))}", flush=True)
+
+
+def part4():
     print("\n# 4. divergence test qp_mu_max: full SQP rounding-decided solves (HPIPM vs literal forms), SQP-RTI changes")
     for cfg, S in (("C4", 2048), ("C2", 1024)):
         lay, b = inputs(cfg, S)

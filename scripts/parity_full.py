@@ -117,8 +117,12 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
     # converged QP solution (a capped QP's step is wherever its stalled interior point stood; with the
     # warm start and in full SQP the next QPs start from it)
     capfree = (got["info"][:, 3] == 0) & (ref["qp_maxiter"] == 0)
-    # the NLP residuals of those solves (a capped step moves the final linearisation point)
-    st_rel = st_relv[same & capfree].max() if (same & capfree).any() else 0.0
+    # the NLP residuals of those solves (a capped step moves the final linearisation point), on the
+    # solves that took the same path (same SQP and IPM iteration counts): a failing solve may end on
+    # another linearisation point with the same exit code (a diverging first QP whose pivot fails at
+    # a rounding-decided iteration, e.g. C5B copy 2489 with HPIPM's profile)
+    samepath = same & capfree & (got["info"][:, 0] == ref["sqp_iter"]) & (got["info"][:, 1] == ref["qp_iter"])
+    st_rel = st_relv[samepath].max() if samepath.any() else 0.0
     dis = np.flatnonzero(~same)
     # failed solves that took the same path on both sides (same RTI and IPM iteration counts) with
     # every accepted step from a converged QP
@@ -188,8 +192,16 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
             "stats_max_rel_diff": float(st_rel),
             "stats_worst": ({"i": int(iw), "gpu": got["stats"][iw].tolist(), "oracle": st[iw].tolist(),
                              "gpu_info": got["info"][iw].tolist(), "exit": int(got["exit"][iw])}
-                            if (same & capfree).any() and (iw := int(np.flatnonzero(same & capfree)[
-                                np.argmax(st_relv[same & capfree])])) >= 0 else None),
+                            if samepath.any() and (iw := int(np.flatnonzero(samepath)[
+                                np.argmax(st_relv[samepath])])) >= 0 else None),
+            # failed solves with the oracle's exit code but another path (SQP / IPM iteration counts), and
+            # how many of them the kernel-forms build follows (the path is then the kernel's arithmetic)
+            "n_failed_other_path": int((bad & ~((got["info"][:, 0] == ref["sqp_iter"]) &
+                                               (got["info"][:, 1] == ref["qp_iter"]))).sum()),
+            "failed_other_path_like_kernel_forms": int((bad & ~((got["info"][:, 0] == ref["sqp_iter"]) &
+                                                              (got["info"][:, 1] == ref["qp_iter"])) &
+                                                        (got["info"][:, 0] == kf["sqp_iter"]) &
+                                                        (got["info"][:, 1] == kf["qp_iter"])).sum()),
             "disagreeing": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
                              "gpu_info": got["info"][i].tolist(), "oracle_sqp": int(ref["sqp_iter"][i]),
                              "oracle_qp_status": int(ref["qp_status"][i])} for i in dis[:20]],
