@@ -100,7 +100,7 @@ def build_instance(layout, out_dir: str, force: bool = False) -> str:
         with open(src, "w") as fh:
             fh.write(text)
     so = os.path.join(out_dir, f"libmpcg_inst_{layout.name}.so")
-    deps = [src, lib_mpcg] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps = [src, lib_mpcg, os.path.join(INCLUDE, "mpcg.h")] + [os.path.join(CSRC, h) for h in HEADERS]
     if force or _stale(so, deps):
         obj = _hipcc_obj(src, os.path.join(out_dir, "mpcg_instance.o"))
         subprocess.run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so + ".tmp", obj, f"-L{PKG}",

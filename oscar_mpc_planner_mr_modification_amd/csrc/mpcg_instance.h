@@ -28,9 +28,13 @@ typedef int (*mpcg_instance_launch)(const mpcg_problem* pr, int batch, const mpc
                                     unsigned long long* stamps, void* workspace);
 /* libmpcg.so's instance table: (model, N, n_lin, n_ell, n_scen, nx) -> launcher, the
  * doubles of one solve's QP memory and the workspace bytes of one solve.  Returns 0 (a
- * shape already present keeps its first launcher). */
-int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
+ * shape already present keeps its first launcher); -3, and the instance stays unknown,
+ * when `abi_version` is not libmpcg.so's MPCG_ABI_VERSION (an instance library compiled
+ * against other sources: mpcg_rejected_instances() counts them). */
+int mpcg_register_instance(int abi_version, int model, int N, int n_lin, int n_ell, int n_scen, int nx, mpcg_instance_launch fn,
                            int qp_mem_size, long long workspace_bytes_per_solve, const char* traits);
+/* instance registrations refused for another ABI since libmpcg.so loaded */
+int mpcg_rejected_instances(void);
 }
 /* the work-queue words at the head of an instance workspace (sqp_kernel) */
 #define MPCG_QUEUE_BYTES 256
@@ -107,7 +111,7 @@ const char* instance_traits() {
 
 template <class C>
 int register_instance() {
-    return mpcg_register_instance(C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM,
+    return mpcg_register_instance(MPCG_ABI_VERSION, C::MODEL, C::N, C::NL, C::NE, C::NS, C::NX, &launch_instance<C>, C::QPM,
                                   (long long)(ws_doubles<C>() * sizeof(double)), instance_traits<C>());
 }
 

@@ -13,6 +13,7 @@
 // DPP trees read back from lane 63 (see the header of mpcg_sqp.h and DESIGN.md §3).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -220,9 +221,20 @@ static int check_problem(const mpcg_problem* pr, int batch, Inst* inst) {
 
 }  // namespace mpcg
 
-extern "C" int mpcg_register_instance(int model, int N, int n_lin, int n_ell, int n_scen, int nx,
+static std::atomic<int> g_rejected_instances{0};
+
+extern "C" int mpcg_rejected_instances(void) { return g_rejected_instances.load(); }
+
+extern "C" int mpcg_register_instance(int abi_version, int model, int N, int n_lin, int n_ell, int n_scen, int nx,
                                       mpcg_instance_launch fn, int qp_mem_size, long long workspace_bytes_per_solve,
                                       const char* traits) {
+    if (abi_version != MPCG_ABI_VERSION) {
+        // a stale instance library: its kernels read another mpcg_problem / workspace layout
+        ++g_rejected_instances;
+        std::fprintf(stderr, "mpcg: instance library compiled against ABI %d, libmpcg.so is ABI %d: rebuild it\n",
+                     abi_version, MPCG_ABI_VERSION);
+        return -3;
+    }
     if (!fn) return -1;
     std::lock_guard<std::mutex> l(mpcg::registry_mutex());
     for (const mpcg::Inst& in : mpcg::registry())

@@ -84,7 +84,12 @@ def load_instances(path: str):
     generated solver's dimensions from then on."""
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path}: build it first (oscar_mpc_planner_mr_modification_amd._build.build_instance)")
-    return C.CDLL(path, mode=C.RTLD_GLOBAL)
+    before = lib.mpcg_rejected_instances()
+    h = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    if lib.mpcg_rejected_instances() != before:
+        raise ImportError(f"{path}: compiled against another ABI than {LIB_PATH}; rebuild it "
+                          "(oscar_mpc_planner_mr_modification_amd._build.build_instance)")
+    return h
 
 
 def supported(pr: MpcgProblem) -> bool:

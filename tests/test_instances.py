@@ -41,6 +41,24 @@ def test_shipped_robot_solvers_have_builtin_instances():
         assert lib.mpcg_supported(C.byref(problem_from_layout(lay))) == 0, lay.name
 
 
+def test_instance_of_another_abi_is_refused():
+    """An instance library compiled against other sources (another MPCG_ABI_VERSION) must not
+    register: its kernels would read another mpcg_problem / workspace layout.  libmpcg.so refuses
+    it and counts it; native.load_instances turns the count into an ImportError."""
+    code = f"""
+import ctypes as C
+lib = C.CDLL({os.path.join(PKG, "libmpcg.so")!r})
+lib.mpcg_register_instance.argtypes = [C.c_int] * 7 + [C.c_void_p, C.c_int, C.c_longlong, C.c_char_p]
+abi = lib.mpcg_abi_version()
+rc = lib.mpcg_register_instance(abi - 1, 0, 25, 3, 0, 0, 4, C.c_void_p(1), 1, 8, b"")
+print(rc, lib.mpcg_rejected_instances())
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["-3", "1"]
+    assert "rebuild" in r.stderr
+
+
 def test_generated_instance_registers_on_load():
     """In a fresh process: the G25 shape is unknown to libmpcg.so until the generated
     instance library is loaded (no GPU call: registration is host code)."""
