@@ -138,27 +138,21 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
-    // 1/t of every row kept in registers when the row state is small (up to 14 slots) on the
-    // three-part instances (C1, C2, C5); the instances with more row slots per lane (C4 20, C3 16)
-    // recompute it, which keeps them out of scratch.  The two-part instances (JS, JD) recompute it
-    // too: the round-2 build that stored 1/t on a two-part instance computed wrong trajectories
-    // and faulted once, and its cause was never named, so the gate stays until it
-    // is.  Measured with the gate lifted (-DMPCG_STORE_IT_ANY; scripts/ab_bench.py,
-    // profiles/r03d_ab_*): JS 42.11 -> 41.39 ms, JD unchanged; full-size parity passed that way
-    // (profiles/r03c_variant_storeit.jsonl).  C5 stored: 20.89 -> 20.68 ms.  Without it C5 is
-    // scratch-free (28 B/lane with it) but slower, 20.69 -> 20.91 (profiles/r03k_ab.jsonl,
-    // MPCG_STORE_IT_MAX=12).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
-// (round 5: 14 -> 13, C5 stops storing it: with the HPIPM profile's cold start and refinement
-// test its stored 1/t pushed the residual and step passes into scratch, 232 -> 80 B/lane)
+    // 1/t of every row kept in registers when the row state is small (up to 13 slots: C1, C2 and the
+    // two-part JS, JD); the instances with more row slots per lane (C5 14, C3 16, C4 20) recompute
+    // it, which keeps them out of scratch.  The two-part instances were gated off from round 2 to
+    // round 5 after a round-2 build that stored 1/t there computed wrong trajectories and faulted
+    // once; round 5 built it again on the shipped sources and ran full-size parity on JS and JD
+    // (2 x 20,480 solves: exit agreement 1.0, max |dx| 2.1e-10, no fault;
+    // profiles/r05f_variant_storeit.jsonl), so the gate is gone.  A/B (profiles/r05f_ab_storeit.jsonl):
+    // JS 52.45 -> 51.73 ms, JD 55.37 -> 55.48.  Round 5: 14 -> 13, C5 stops storing it (with the HPIPM
+    // profile's cold start and refinement test its stored 1/t pushed the residual and step passes into
+    // scratch, 232 -> 80 B/lane; profiles/r05c_ab_st14_C5.jsonl).  MPCG_STORE_IT_MAX=0 recomputes it
+    // everywhere.
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 13
 #endif
-#ifdef MPCG_STORE_IT_ANY
-    static constexpr bool STORE_IT_PARTS_OK = true;
-#else
-    static constexpr bool STORE_IT_PARTS_OK = PARTS == 3;
-#endif
-    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX && STORE_IT_PARTS_OK;
+    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
     // box bounds selected per use instead of held in registers (LaneBounds; MPCG_BOUNDS_SEL=1, A/B
     // only): C2 went into scratch with it (0 -> 68 B/lane), C3 unchanged, and C4 (148 -> 132 B/lane
     // of scratch) measured 50.75 vs 50.72 ms in two alternating repetitions (profiles/r03k_ab.jsonl)
@@ -383,7 +377,7 @@ __host__ __device__ constexpr size_t ws_doubles() {
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
 // production build compiles them out).  Read shares, not absolute times.
 #ifdef MPCG_STAMPS
-#define MPCG_NSTAMP 20
+#define MPCG_NSTAMP 24
 #define STAMP_DECL unsigned long long st_acc_[MPCG_NSTAMP] = {}, st_t0_ = 0, st_l_ = 0;
 #define STAMP_BEGIN() do { __syncthreads(); st_t0_ = __builtin_amdgcn_s_memtime(); st_l_ = st_t0_; } while (0)
 #define STAMP_END(i) do { __syncthreads(); st_acc_[i] += __builtin_amdgcn_s_memtime() - st_t0_; } while (0)

@@ -1,60 +1,63 @@
-"""Bit-for-bit comparison of two kernel builds on the bench batch of a config (GPU).
+"""Bit comparison of kernel builds (GPU box; test infrastructure): the bench batch of each config
+through two or more libmpcg.so builds (MPCG_LIB, one child process each), outputs compared exactly.
 
-    python scripts/bitcmp.py dump <out.npz> --config C2     (MPCG_LIB selects the build)
-    python scripts/bitcmp.py cmp <a.npz> <b.npz>
-
-A transformation that keeps every floating-point operation of the solve (same operations, other
-lanes or another order of independent work) must give identical outputs."""
+    python scripts/bitcmp.py --libs prod,build/ab/x/libmpcg.so --configs C2,C4 [--profile hpipm]
+"""
 import argparse
+import json
 import os
+import subprocess
 import sys
-
-import numpy as np
+import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def dump(path, config, scenes):
+def child(cfg, profile, out):
+    import numpy as np
     import torch
 
     from oscar_mpc_planner_mr_modification_amd import native
-
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    from parity_full import inputs
-
-    lay, b = inputs(config, scenes)
-    dev = torch.device("cuda:0")
-    params, warm, xinit = b.params, b.warm, b.xinit
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    out = native.solve_batch_device(native.problem_from_layout(lay), t(params), t(warm), t(xinit))
-    torch.cuda.synchronize()
-    np.savez(path, **{k: v.cpu().numpy() for k, v in out.items()})
-    print(path, {k: v.shape for k, v in out.items()})
+    from parity_full import DEFAULT_SCENES, inputs
+    lay, b = inputs(cfg, DEFAULT_SCENES[cfg])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")  # noqa: E731
+    o = native.solve_batch_device(native.problem_from_layout(lay, qp_profile=profile), t(b.params), t(b.warm),
+                                  t(b.xinit))
+    np.savez(out, **{k: v.cpu().numpy() for k, v in o.items()})
 
 
-def cmp(a, b):
-    A, B = np.load(a), np.load(b)
-    bad = 0
-    for k in A.files:
-        x, y = A[k], B[k]
-        same = x.shape == y.shape and np.array_equal(x.view(np.uint8), y.view(np.uint8))
-        if not same:
-            bad += 1
-            d = np.abs(x.astype(np.float64) - y.astype(np.float64))
-            print(k, "DIFFERS: max abs", float(np.nanmax(d)), "entries", int((x != y).sum()))
-    print("bit-identical" if bad == 0 else f"{bad} arrays differ")
-    return bad
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default="prod")
+    ap.add_argument("--configs", default="C2")
+    ap.add_argument("--profile", default="hpipm")
+    ap.add_argument("--child", nargs=3, help=argparse.SUPPRESS)
+    a = ap.parse_args()
+    if a.child:
+        child(*a.child)
+        return
+    import numpy as np
+    libs = [os.path.join(ROOT, "oscar_mpc_planner_mr_modification_amd", "libmpcg.so") if x == "prod" else
+            os.path.join(ROOT, x) for x in a.libs.split(",")]
+    tmp = tempfile.mkdtemp()
+    for cfg in a.configs.split(","):
+        outs = []
+        for i, lib in enumerate(libs):
+            f = os.path.join(tmp, f"{cfg}_{i}.npz")
+            subprocess.run([sys.executable, os.path.abspath(__file__), "--child", cfg, a.profile, f],
+                           env=dict(os.environ, MPCG_LIB=lib), check=True)
+            outs.append(np.load(f))
+        ref = outs[0]
+        for lib, o in zip(libs[1:], outs[1:]):
+            rec = {"config": cfg, "lib": os.path.relpath(lib, ROOT), "profile": a.profile}
+            for k in ref.files:
+                x, y = ref[k], o[k]
+                same = np.array_equal(x, y, equal_nan=True) if x.dtype.kind == "f" else np.array_equal(x, y)
+                rec[k] = "equal" if same else float(np.nanmax(np.abs(x.astype(np.float64) - y.astype(np.float64))))
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
-    ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["dump", "cmp"])
-    ap.add_argument("files", nargs="+")
-    ap.add_argument("--config", default="C2")
-    ap.add_argument("--scenes", type=int, default=512)
-    a = ap.parse_args()
-    if a.mode == "dump":
-        dump(a.files[0], a.config, a.scenes)
-    else:
-        sys.exit(1 if cmp(*a.files) else 0)
+    main()

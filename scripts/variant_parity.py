@@ -4,9 +4,9 @@
     python scripts/variant_parity.py --run storeit     # GPU: JS / JD full size with stored 1/t
     python scripts/variant_parity.py --run bike3       # GPU: the N 10 bicycle shape with three parts
 
-storeit: -DMPCG_STORE_IT_ANY -- the two-part instances (JS, JD) keep 1/t of every row in
-         registers (round 3: the PARTS == 3 gate of Cfg::STORE_IT lifted -- since then the
-         default, so this variant equals the production build);
+storeit: -DMPCG_STORE_IT_ANY -- round 5's parity run of the two-part instances (JS, JD) keeping
+         1/t of every row in registers (profiles/r05f_variant_storeit.jsonl); the gate it lifted
+         is gone since, so this variant now equals the production build;
 bike3:   -DMPCG_PARTS_BIKE=3 -- the bicycle's N 10 test shape with three lane parts per stage.
 Each variant runs in a child process with MPCG_LIB pointing at it."""
 import argparse
