@@ -23,7 +23,7 @@ for s in "$@"; do
     sqp)
       step sqp 900 gpurun_out/${tag}_sqp_parity.jsonl python -u scripts/parity_full.py --configs C2,C1,C4 --ws 2 --warm-first 0 --solver-type SQP ;;
     tests)
-      step tests 1500 gpurun_out/${tag}_gpu_tests.log python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ;;
+      step tests 1500 gpurun_out/${tag}_gpu_tests.log python -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread ;;
     smoke)
       step smoke 300 gpurun_out/${tag}_smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
