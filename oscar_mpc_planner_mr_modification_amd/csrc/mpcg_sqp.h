@@ -145,14 +145,18 @@ struct Cfg {
     // once; round 5 built it again on the shipped sources and ran full-size parity on JS and JD
     // (2 x 20,480 solves: exit agreement 1.0, max |dx| 2.1e-10, no fault;
     // profiles/r05f_variant_storeit.jsonl), so the gate is gone.  A/B (profiles/r05f_ab_storeit.jsonl):
-    // JS 52.45 -> 51.73 ms, JD 55.37 -> 55.48.  Round 5: 14 -> 13, C5 stops storing it (with the HPIPM
-    // profile's cold start and refinement test its stored 1/t pushed the residual and step passes into
-    // scratch, 232 -> 80 B/lane; profiles/r05c_ab_st14_C5.jsonl).  MPCG_STORE_IT_MAX=0 recomputes it
-    // everywhere.
+    // JS 52.45 -> 51.73 ms, JD 55.37 -> 55.48 with twice the scratch (100 -> 204 B/lane, HBM traffic
+    // 8.9x the algorithmic bytes): two-part instances store it up to 12 slots (JS), JD (13) recomputes.
+    // Round 5: 14 -> 13, C5 stops storing it (with the HPIPM profile's cold start and refinement test
+    // its stored 1/t pushed the residual and step passes into scratch, 232 -> 80 B/lane;
+    // profiles/r05c_ab_st14_C5.jsonl).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 13
 #endif
-    static constexpr bool STORE_IT = SLOTS <= MPCG_STORE_IT_MAX;
+#ifndef MPCG_STORE_IT_MAX2
+#define MPCG_STORE_IT_MAX2 12
+#endif
+    static constexpr bool STORE_IT = SLOTS <= (PARTS == 3 ? MPCG_STORE_IT_MAX : MPCG_STORE_IT_MAX2);
     // box bounds selected per use instead of held in registers (LaneBounds; MPCG_BOUNDS_SEL=1, A/B
     // only): C2 went into scratch with it (0 -> 68 B/lane), C3 unchanged, and C4 (148 -> 132 B/lane
     // of scratch) measured 50.75 vs 50.72 ms in two alternating repetitions (profiles/r03k_ab.jsonl)
