@@ -366,11 +366,11 @@ __host__ __device__ constexpr size_t gfh_doubles() {
     return lds_gfh<C>() ? (size_t)C::N * C::NFR * C::NFC + (size_t)(C::N + 1) * C::NHP : 0;
 }
 // doubles of one solve's iterative-refinement scratch (qp_itref_corr_max, the rare path: the
-// unrefined direction's step [N+1][NZ] and dynamics multipliers [N][NX], and the refinement's
-// dynamics right-hand side [N][NX])
+// unrefined direction's step [N+1][NZ] and dynamics multipliers [N][NX], and -- LEAN -- the iterate's
+// QP step [N+1][NZ] while S.dz holds the trial point)
 template <class C>
 __host__ __device__ constexpr size_t itref_doubles() {
-    return (size_t)(C::N + 1) * C::NZ + 2 * (size_t)C::N * C::NX;
+    return 2 * (size_t)(C::N + 1) * C::NZ + (size_t)C::N * C::NX;
 }
 // one solve's global workspace: the GFH blocks, then the refinement scratch
 template <class C>
