@@ -136,11 +136,19 @@ def spawn_ranks(n, argv):
     return subprocess.call(cmd, env=dict(os.environ))
 
 
-def spawn_check(world):
-    """--spawn-check (CPU test of the rank spawning): every rank joins a gloo group and counts
-    the ranks; rank 0 prints one JSON line."""
+def spawn_check(world, config="C4", per_rank=None):
+    """--spawn-check (CPU test of the rank spawning and of the step's collective): every rank joins a
+    gloo group and counts the ranks, then runs the winner all-gather the timed step runs at this
+    world size on host tensors: the weak-scaling shards of `config` (per_rank scenes each, the
+    bench's default per GPU: C4 2048, i.e. BASELINE config 4's 16,384 scenes over 8 ranks) into the
+    preallocated result buffer, and an uneven sharding of the same total plus 3 scenes (ranks with
+    one scene fewer; distributed.gather_winners(total=...)).  Each record holds its global scene
+    index, so rank 0 checks both gathers exactly; it prints one JSON line."""
     import torch
     import torch.distributed as dist
+
+    from oscar_mpc_planner_mr_modification_amd.distributed import gather_winners, shard, winner_width
+    from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
 
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
@@ -148,9 +156,29 @@ def spawn_check(world):
     t = torch.ones(1)
     if world > 1:
         dist.all_reduce(t)
+    lay = config_layout(config)
+    S = per_rank or DEFAULT_SCENES[config]
+    w = winner_width(lay.N, lay.nx, lay.nu)
+
+    def records(first, count):
+        # scene s: column j holds s + j / w (distinct per scene and column, exact in f64)
+        s = torch.arange(first, first + count, dtype=torch.float64)[:, None]
+        return s + torch.arange(w, dtype=torch.float64)[None, :] / w
+
+    even = torch.empty((S * world, w), dtype=torch.float64)
+    got_even = gather_winners(records(rank * S, S), world, out=even)
+    total = S * world + 3
+    first, count = shard(total, world, rank)
+    got_uneven = gather_winners(records(first, count), world, total=total)
+    ok = bool(torch.equal(got_even, records(0, S * world)) and torch.equal(got_uneven, records(0, total)))
+    if world > 1:
+        flag = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item() == 1.0)
     if rank == 0:
         print(json.dumps({"spawn_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
-                          "local_ranks": world}))
+                          "local_ranks": world, "config": config, "scenes_per_rank": S,
+                          "gather_even_scenes": S * world, "gather_uneven_scenes": total, "gather_ok": ok}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -415,8 +443,11 @@ def oracle_check(wl, orc, lo, hi, exit_h, xt_h, info_h, nthreads):
     # converged QP (no max-iter QP): their last iterates must agree like successful ones
     path = (same & (ex != 1) & (inf[:, 0] == ref["sqp_iter"]) & (inf[:, 1] == ref["qp_iter"]) &
             (inf[:, 3] == 0) & (ref["qp_maxiter"] == 0))
+    # the oracle's rare interior-point passes on these solves (centring re-solves, refinement solves)
+    # and its IPM iterations: the rates the executed-work flop count uses (flopmodel.solve_ops_executed)
+    rare = np.array([ref["qp_iter"].sum(), ref["qp_center"].sum(), ref["qp_itref"].sum()], dtype=np.float64)
     return (sec, float(dx[ok].max()) if ok.any() else 0.0, float(dx[path].max()) if path.any() else 0.0,
-            int(same.sum()), len(ex))
+            int(same.sum()), len(ex), rare)
 
 
 def native_problem(lay, args, profile):
@@ -471,7 +502,7 @@ def main():
                  f"`python -m torch.distributed.run --nnodes=1 --nproc-per-node {args.gpus} --master-addr "
                  f"127.0.0.1 bench.py --gpus {args.gpus} ...`, or plain `bench.py --gpus {args.gpus}`)")
     if args.spawn_check:
-        return spawn_check(world)
+        return spawn_check(world, args.config, args.scenes)
 
     import torch
     import torch.distributed as dist
@@ -571,7 +602,11 @@ def main():
     # figure with SURVEY.md §8(d)'s algorithmic bytes per solve
     from oscar_mpc_planner_mr_modification_amd import flopmodel
 
-    flop = float(flopmodel.solve_ops(lay, info_h).sum())
+    # the executed algorithm: the base Mehrotra count plus, on HPIPM's profile,
+    # the refinement test of every IPM iteration; the rare centring / refinement solves are added by
+    # executed_flops below at the rates of the oracle's run on a sample of the batch (none without it)
+    flop_base = float(flopmodel.solve_ops(lay, info_h).sum())
+    flop = float(flopmodel.solve_ops_executed(lay, info_h, args.qp_profile).sum())
     tflops = flop / (kern_ms * 1e-3) / 1e12
     bps = algorithmic_bytes_per_solve(lay)
     achieved = bps * B / (kern_ms * 1e-3) / 1e9
@@ -579,10 +614,26 @@ def main():
     roofline = {"bound": "fp64_valu", "achieved": round(tflops, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": tflops / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
                 "kernel": "sqp_kernel", "kernel_ms": round(kern_ms, 4),
-                "flop_per_solve": round(flop / B), "flop_model": "analytic (flopmodel.py) x executed iterations",
+                "flop_per_solve": round(flop / B),
+                "flop_model": ("analytic (flopmodel.solve_ops_executed) x executed iterations: the Mehrotra iteration, "
+                               "HPIPM's refinement test per IPM iteration" if args.qp_profile == "hpipm" else
+                               "analytic (flopmodel.solve_ops) x executed iterations"),
+                "flop_per_solve_base": round(flop_base / B),
+                "frac_base": (flop_base / (kern_ms * 1e-3) / 1e12) / FP64_VALU_PEAK_TFLOPS,
                 "hbm": {"achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "bytes_per_solve": bps, "traffic": traffic},
                 "counters": counters}
+    def executed_flops(rare, source):
+        """add the rare interior-point passes at the oracle sample's rates per IPM iteration"""
+        if args.qp_profile != "hpipm" or rare[0] <= 0:
+            return
+        cr, ir = rare[1] / rare[0], rare[2] / rare[0]
+        fl = float(flopmodel.solve_ops_executed(lay, info_h, "hpipm", cr, ir).sum())
+        tf = fl / (kern_ms * 1e-3) / 1e12
+        roofline.update({"achieved": round(tf, 3), "frac": tf / FP64_VALU_PEAK_TFLOPS, "flop_per_solve": round(fl / B)})
+        roofline["flop_model"] += (f", centring re-solves ({cr:.4f} per IPM iteration) and refinement solves "
+                                   f"({ir:.4f}) at {source} rates")
+
     if f64:
         # cross-check from the PMC pass on the same sources: issued fp64 FLOP/s of the solve kernel
         # (SQ_INSTS_VALU_*_F64 x 64 lanes, masked lanes included) and that figure weighted by the
@@ -650,12 +701,15 @@ def main():
         if world == 1:
             # CPU baseline: chunks of the same batch until ~cpu_seconds of CPU work, checked on the way
             done, t_cpu, dx_ok, dx_fail, agree, compared = 0, 0.0, 0.0, 0.0, 0, 0
+            rare = np.zeros(3)
             while done < B and t_cpu < args.cpu_seconds:
                 hi = min(B, done + CHECK_CHUNK)
-                sec, a, f, g, n = oracle_check(wl, orc, done, hi, exit_h, xt_h, info_h, threads)
+                sec, a, f, g, n, rr = oracle_check(wl, orc, done, hi, exit_h, xt_h, info_h, threads)
                 t_cpu += sec
                 dx_ok, dx_fail, agree, compared = max(dx_ok, a), max(dx_fail, f), agree + g, compared + n
+                rare += rr
                 done = hi
+            executed_flops(rare, f"the oracle's on the first {done} solves of this batch")
 
             def rate(n, nthreads):
                 prm, wrm, xin = wl.host_inputs(0, min(n, B))
@@ -679,7 +733,8 @@ def main():
         else:
             # every rank checks a sample of its own shard; reduced over ranks
             n = min(RANK_SAMPLE, B)
-            _, dx_ok, dx_fail, agree, compared = oracle_check(wl, orc, 0, n, exit_h, xt_h, info_h, threads)
+            _, dx_ok, dx_fail, agree, compared, rare = oracle_check(wl, orc, 0, n, exit_h, xt_h, info_h, threads)
+            executed_flops(rare, f"the oracle's on this rank's first {n} solves")
             t = torch.tensor([dx_ok, dx_fail, agree, compared, 1.0], dtype=torch.float64, device=dev)
             tm = t.clone()
             all_reduce_(tm, dist.ReduceOp.MAX)

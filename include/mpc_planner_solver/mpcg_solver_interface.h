@@ -23,6 +23,40 @@
 #include "mpc_planner_solver/state.h"
 #include "mpcg.h"
 
+// The reference header's short dimension names (acados_solver_interface.h:20-47), over the generated
+// SOLVER_* values, for code compiled against that header.  MPCG_NO_DIM_MACROS leaves them out where a
+// translation unit has its own NX / NU / ... identifiers.
+#ifndef MPCG_NO_DIM_MACROS
+#define NX SOLVER_NX
+#define NZ SOLVER_NZ
+#define NU SOLVER_NU
+#define NBX SOLVER_NBX
+#define NBX0 SOLVER_NBX0
+#define NBU SOLVER_NBU
+#define NSBX SOLVER_NSBX
+#define NSBU SOLVER_NSBU
+#define NSH SOLVER_NSH
+#define NSG SOLVER_NSG
+#define NSPHI SOLVER_NSPHI
+#define NSHN SOLVER_NSHN
+#define NSGN SOLVER_NSGN
+#define NSPHIN SOLVER_NSPHIN
+#define NSBXN SOLVER_NSBXN
+#define NS SOLVER_NS
+#define NSN SOLVER_NSN
+#define NG SOLVER_NG
+#define NBXN SOLVER_NBXN
+#define NGN SOLVER_NGN
+#define NY0 SOLVER_NY0
+#define NY SOLVER_NY
+#define NYN SOLVER_NYN
+#define NH SOLVER_NH
+#define NPHI SOLVER_NPHI
+#define NHN SOLVER_NHN
+#define NPHIN SOLVER_NPHIN
+#define NR SOLVER_NR
+#endif
+
 namespace MPCPlanner {
 
 // Input block of one solve (acados_solver_interface.h:51-90).

@@ -44,7 +44,7 @@ namespace mpcg {
 // grid of a work-queue launch: the workgroups the stream's device holds at once (occupancy x
 // CUs), at most one per problem; cached per device.  MPCG_QUEUE_GRID_PER_CU (A/B only) sets the
 // workgroups per CU.
-template <class C, bool FULL>
+template <class C, bool FULL, int PROF>
 int queue_grid(int batch, hipStream_t stream) {
     constexpr int MAXDEV = 64;
     static std::atomic<int> resident[MAXDEV];  // 0: not yet asked, -1: no answer
@@ -61,7 +61,7 @@ int queue_grid(int batch, hipStream_t stream) {
 #else
             int cur = 0;
             const bool sw = hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL>, 64, 0) != hipSuccess)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL, PROF>, 64, 0) != hipSuccess)
                 per_cu = 0;
             if (sw) (void)hipSetDevice(cur);
 #endif
@@ -73,25 +73,40 @@ int queue_grid(int batch, hipStream_t stream) {
     return r > 0 && r < batch ? r : batch;
 }
 
+template <class C, bool FULL, int PROF>
+void launch_kernel(const mpcg_problem* pr, int batch, const mpcg_io* io, hipStream_t st, unsigned long long* stamps,
+                   double* gws, unsigned* queue) {
+    hipLaunchKernelGGL((sqp_kernel<C, FULL, PROF>), dim3(queue ? queue_grid<C, FULL, PROF>(batch, st) : batch),
+                       dim3(64), 0, st, *pr, batch, *io, stamps, gws, queue);
+}
+
 template <class C>
 int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* stream, unsigned long long* stamps,
                     void* workspace) {
-    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync);
-    // the full variant only when the call needs QP memory, the warm start, the residuals or
-    // the full SQP
-    if (ws_doubles<C>() > 0 && !workspace) return (int)hipErrorInvalidValue;
-    unsigned* queue = C::QUEUE ? (unsigned*)workspace : nullptr;
+    // exactly one wavefront per workgroup: the kernel's lane exchanges rely on it (wave_sync).
+    // The workspace (MPCG_QUEUE_BYTES + batch x the instance's bytes per solve) is required where it
+    // is read: the GFH stage blocks, and the refinement scratch when the profile refines
+    // (qp_itref_corr_max > 0, HPIPM's profile); a robust-profile call of an instance without GFH may
+    // pass NULL (one workgroup per problem then, without the work queue)
+    if ((gfh_doubles<C>() > 0 || (pr->qp_itref_corr_max > 0 && itref_doubles<C>() > 0)) && !workspace)
+        return (int)hipErrorInvalidValue;
+    unsigned* queue = C::QUEUE && workspace ? (unsigned*)workspace : nullptr;
     double* gws = workspace ? (double*)((char*)workspace + MPCG_QUEUE_BYTES) : nullptr;
     const hipStream_t st = (hipStream_t)stream;
     // the queue counter starts at zero for every launch, whatever an earlier launch on this
     // workspace left behind (one that died mid-way included): a 256-byte memset on the stream
     if (queue && hipMemsetAsync(queue, 0, MPCG_QUEUE_BYTES, st) != hipSuccess) return (int)hipGetLastError();
-    if (io->stats || io->qp_in || io->qp_out || needs_full(*pr))
-        hipLaunchKernelGGL((sqp_kernel<C, true>), dim3(queue ? queue_grid<C, true>(batch, st) : batch), dim3(64), 0,
-                           st, *pr, batch, *io, stamps, gws, queue);
+    // the full variant only when the call needs QP memory, the warm start, the residuals or the full
+    // SQP; the lean one specialised on the call's interior-point profile (qp_profile_kind), and a lean
+    // call whose switches match neither profile on the full variant's run-time switches (without QP
+    // memory, residuals or warm start the full variant runs the lean variant's operations)
+    const int prof = qp_profile_kind(*pr);
+    if (io->stats || io->qp_in || io->qp_out || needs_full(*pr) || prof == PROF_RUNTIME)
+        launch_kernel<C, true, PROF_RUNTIME>(pr, batch, io, st, stamps, gws, queue);
+    else if (prof == PROF_HPIPM)
+        launch_kernel<C, false, PROF_HPIPM>(pr, batch, io, st, stamps, gws, queue);
     else
-        hipLaunchKernelGGL((sqp_kernel<C, false>), dim3(queue ? queue_grid<C, false>(batch, st) : batch), dim3(64),
-                           0, st, *pr, batch, *io, stamps, gws, queue);
+        launch_kernel<C, false, PROF_ROBUST>(pr, batch, io, st, stamps, gws, queue);
     return (int)hipGetLastError();
 }
 

@@ -138,23 +138,27 @@ struct Cfg {
     static constexpr int BVS = (NZ + PARTS - 1) / PARTS;
     static constexpr int HS = (NH + PARTS - 1) / PARTS;
     static constexpr int SLOTS = 2 * BVS + HS;
-    // 1/t of every row kept in registers when the row state is small (up to 13 slots: C1, C2 and the
-    // two-part JS, JD); the instances with more row slots per lane (C5 14, C3 16, C4 20) recompute
-    // it, which keeps them out of scratch.  The two-part instances were gated off from round 2 to
-    // round 5 after a round-2 build that stored 1/t there computed wrong trajectories and faulted
-    // once; round 5 built it again on the shipped sources and ran full-size parity on JS and JD
-    // (2 x 20,480 solves: exit agreement 1.0, max |dx| 2.1e-10, no fault;
-    // profiles/r05f_variant_storeit.jsonl), so the gate is gone.  A/B (profiles/r05f_ab_storeit.jsonl):
-    // JS 52.45 -> 51.73 ms, JD 55.37 -> 55.48 with twice the scratch (100 -> 204 B/lane, HBM traffic
-    // 8.9x the algorithmic bytes): two-part instances store it up to 12 slots (JS), JD (13) recomputes.
-    // Round 5: 14 -> 13, C5 stops storing it (with the HPIPM profile's cold start and refinement test
-    // its stored 1/t pushed the residual and step passes into scratch, 232 -> 80 B/lane;
-    // profiles/r05c_ab_st14_C5.jsonl).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
+    // 1/t of every row kept in registers when the row state is small (up to 13 slots on the three-part
+    // instances: C1, C2); C5 (14 slots), C3 (16) and C4 (20) recompute it, which keeps them out of
+    // scratch.  Round 5: 14 -> 13, C5 stops storing it (with the HPIPM profile's cold start and
+    // refinement test its stored 1/t pushed the residual and step passes into scratch, 232 -> 80
+    // B/lane; profiles/r05c_ab_st14_C5.jsonl).  MPCG_STORE_IT_MAX=0 recomputes it everywhere.
+    // Two-part instances (JS, JD) recompute it: a round-2 build that stored 1/t there computed wrong
+    // trajectories and faulted once, and that fault's cause was never named (its build no longer
+    // exists).  Round 5 built the stored form again on the shipped sources, ran full-size parity on JS
+    // and JD without a fault (profiles/r05f_variant_storeit.jsonl) and lifted the gate for a 1.4 % JS
+    // gain (52.45 -> 51.73 ms, profiles/r05f_ab_storeit.jsonl); one clean run shows the fault did not
+    // recur, not that its cause is gone, so round 6 restores the gate.  -DMPCG_STORE_IT_ANY
+    // (or MPCG_STORE_IT_MAX2 > 0) builds the stored form on two-part instances for A/B runs only.
 #ifndef MPCG_STORE_IT_MAX
 #define MPCG_STORE_IT_MAX 13
 #endif
 #ifndef MPCG_STORE_IT_MAX2
+#ifdef MPCG_STORE_IT_ANY
 #define MPCG_STORE_IT_MAX2 12
+#else
+#define MPCG_STORE_IT_MAX2 0
+#endif
 #endif
     static constexpr bool STORE_IT = SLOTS <= (PARTS == 3 ? MPCG_STORE_IT_MAX : MPCG_STORE_IT_MAX2);
     // box bounds selected per use instead of held in registers (LaneBounds; MPCG_BOUNDS_SEL=1, A/B
@@ -651,6 +655,23 @@ __host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
     return pr.nlp_solver == MPCG_NLP_SQP || (pr.qp_warm_start == 2 && pr.qp_warm_first);
 }
 
+// The interior point's profile (mpcg_problem_set_qp_profile) as a template parameter of
+// the kernel: the lean kernels are compiled once per profile with its structural switches (the primal box
+// move, the conditional corrector, the corrector's refinement, sigma's clip, the exit order, the divergence
+// test) as constants, so neither profile carries the other's code or its live state.  PROF_RUNTIME reads
+// them from mpcg_problem (the FULL variant, and a lean call with a combination of switches that is neither
+// profile).  The continuous constants (mu0, thr0, t_min, mu_max) stay run-time arguments.
+enum { PROF_RUNTIME = 0, PROF_HPIPM = 1, PROF_ROBUST = 2 };
+__host__ __device__ inline int qp_profile_kind(const mpcg_problem& pr) {
+    if (pr.qp_init_move == 1 && pr.qp_cond_pred_corr == 1 && pr.qp_itref_corr_max == 2 && pr.qp_sigma_clip == 0 &&
+        pr.qp_maxit_first == 1 && !(pr.qp_mu_max > 0.0))
+        return PROF_HPIPM;
+    if (pr.qp_init_move == 0 && pr.qp_cond_pred_corr == 0 && pr.qp_itref_corr_max == 0 && pr.qp_sigma_clip == 1 &&
+        pr.qp_maxit_first == 0 && pr.qp_mu_max > 0.0)
+        return PROF_ROBUST;
+    return PROF_RUNTIME;
+}
+
 // FULL: the variant with the capsule's QP memory (mpcg_io.qp_in / qp_out), the HPIPM warm
 // start (pr.qp_warm_start == 2) and the NLP residuals of every linearisation
 // (mpcg_io.stats; the drop-in's AcadosInfo).  The lean variant (FULL = false: cold
@@ -665,7 +686,7 @@ __host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
 #define MPCG_KERNEL_ATTR __launch_bounds__(64, 1)
 #endif
 // one solve `sol` on the calling wavefront (the body of sqp_kernel)
-template <class C, bool FULL>
+template <class C, bool FULL, int PROF>
 __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io,
                                           unsigned long long* __restrict__ stamps, double* __restrict__ gws,
                                           const int sol) {
@@ -681,7 +702,7 @@ __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io
 // solve of the whole batch (the tail).  Every wave leaves the loop on its first
 // ticket >= batch.  launch_instance zeroes the queue words on the launch stream before every
 // launch, so no launch depends on how the previous one on the same workspace ended.
-template <class C, bool FULL = false>
+template <class C, bool FULL = false, int PROF = PROF_RUNTIME>
 __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps,
                                                     double* __restrict__ gws, unsigned* __restrict__ queue) {
@@ -706,7 +727,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
             return t < (unsigned)batch ? (int)t : batch;
         };
         for (int sol = q ? next() : (int)blockIdx.x; sol < batch; sol = q ? next() : batch) {
-            sqp_solve<C, FULL>(pr, batch, io, stamps, gws, sol);
+            sqp_solve<C, FULL, PROF>(pr, batch, io, stamps, gws, sol);
             wave_sync();
         }
     }

@@ -116,6 +116,57 @@ def linearisation_ops(lay, rk_steps: int | None = None) -> int:
 
 def solve_ops(lay, info) -> np.ndarray:
     """Per-solve fp64 operations from the kernel's executed counts: info[:,0] SQP-RTI iterations
-    (one linearisation each), info[:,1] interior-point iterations (summed over the QPs)."""
+    (one linearisation each), info[:,1] interior-point iterations (summed over the QPs).  The base
+    count: the Mehrotra iteration without HPIPM's extras (solve_ops_executed adds them)."""
     info = np.asarray(info)
     return info[:, 0].astype(np.float64) * linearisation_ops(lay) + info[:, 1].astype(np.float64) * ipm_iteration_ops(lay)
+
+
+def _rows_of_stage(lay, k):
+    return [1] * (2 * lay.nu) + ([1] * (2 * lay.nx) + _row_nnz(lay) if k >= 1 else [])
+
+
+def refinement_test_ops(lay) -> int:
+    """HPIPM's itref_corr_max > 0: after every corrector, the direction's linear KKT
+    residual against its tolerance -- stationarity at the trial point (H (dz + ddz) + g + box and row
+    multiplier sums + [B A]'pi_new - pi_new,prev), the dynamics rows at the trial point and per row
+    the complementarity part l dt + t dl + rc; then one compare per component."""
+    N, nu, nx = lay.N, lay.nu, lay.nx
+    nz = nu + nx
+    ops = 0
+    for k in range(N):
+        rows = _rows_of_stage(lay, k)
+        m, sc = len(rows), sum(rows)
+        ops += nz + (nz * (nz + 1) + nz) + 2 * nx * nz + nx + 2 * sc + nz  # trial point, stationarity
+        ops += nz + 2 * nx * nz + 2 * nx + nx                              # dynamics at the trial point
+        ops += 8 * m + 2 * m                                               # row steps, complementarity
+    return int(ops)
+
+
+def newton_solve_ops(lay) -> int:
+    """one Newton solve with the factorisation at hand (a centring pass of the conditional
+    predictor-corrector re-solves the corrector's system): the gradient, both vector passes, the
+    feedback, the row steps and the step length (the `sol` term of ipm_iteration_ops_by_part)."""
+    return int(ipm_iteration_ops_by_part(lay)["newton_solves"] // 2)
+
+
+def refinement_solve_ops(lay) -> int:
+    """one refinement step: the right-hand side from the linear residual (refinement_test_ops' terms
+    with the Newton gradient formed from them) and one Newton solve"""
+    return int(refinement_test_ops(lay) + sum(2 * c + 3 for k in range(lay.N) for c in _rows_of_stage(lay, k)) +
+               newton_solve_ops(lay))
+
+
+def solve_ops_executed(lay, info, profile="hpipm", center_per_ipm=0.0, itref_per_ipm=0.0) -> np.ndarray:
+    """The operations of the interior point that actually runs: solve_ops plus,
+    under HPIPM's profile, the refinement test of every IPM iteration, and the rare passes -- centring
+    re-solves of the conditional predictor-corrector and refinement solves -- at the given rates per
+    IPM iteration (the kernel does not count them; bench.py takes them from the oracle run on a sample
+    of the same batch, whose IPM path the GPU's follows solve for solve)."""
+    info = np.asarray(info)
+    ipm = info[:, 1].astype(np.float64)
+    ops = solve_ops(lay, info)
+    if profile == "hpipm":
+        ops = ops + ipm * (refinement_test_ops(lay) + center_per_ipm * newton_solve_ops(lay) +
+                           itref_per_ipm * refinement_solve_ops(lay))
+    return ops

@@ -56,8 +56,9 @@ def main():
     ap.add_argument("--warm-first", type=int, default=0)
     ap.add_argument("--solver-type", default="SQP_RTI", choices=("SQP_RTI", "SQP"))
     ap.add_argument("--variant", default="lean", choices=("lean", "full"))
-    ap.add_argument("--qp-profile", default="robust", choices=("hpipm", "robust"),
-                    help="the interior point's profile (DESIGN.md §2.2) of both sides")
+    ap.add_argument("--qp-profile", default="hpipm", choices=("hpipm", "robust"),
+                    help="the interior point's profile (DESIGN.md §2.2) of both sides; the product default "
+                         "(native_spec.DEFAULT_OPTIONS) is HPIPM's")
     ap.add_argument("--forms", default="hpipm", choices=("hpipm", "literal", "kernel"),
                     help="the oracle build to trace (oracle/mpcg_oracle.c \"Arithmetic forms\")")
     args = ap.parse_args()

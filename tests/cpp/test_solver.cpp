@@ -23,6 +23,12 @@
 
 using namespace MPCPlanner;
 
+// the reference header's short dimension names (acados_solver_interface.h:20-47) over the generated values
+static_assert(NX == SOLVER_NX && NU == SOLVER_NU && NH == SOLVER_NH && NZ == 0, "dimension macros");
+static_assert(NBX == NX && NBX0 == NX && NBU == NU, "box bounds on every state and input");
+static_assert(NS == 0 && NSN == 0 && NG == 0 && NY == 0 && NHN == 0 && NBXN == 0 && NR == 0, "no soft / LS / terminal");
+static_assert(sizeof(AcadosParameters::x0) == sizeof(double) * (NU + NX) * (SOLVER_N + 1), "x0 layout");
+
 static int g_fail = 0;
 #define CHECK(c)                                                                   \
     do {                                                                           \

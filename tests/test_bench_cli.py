@@ -21,6 +21,25 @@ def test_gpus_flag_spawns_its_own_ranks():
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["ranks_seen"] == 2 and line["n_gpus"] == 2
+    assert line["gather_ok"], line
+
+
+def test_gpus_8_spawns_eight_ranks_and_gathers_the_c4_shards():
+    """the width the driver's scaling run uses: `bench.py --gpus 8` (no launcher) starts eight ranks,
+    and the step's winner all-gather is exact over BASELINE config 4's 16,384 scenes (2,048 per rank,
+    N 30 records) and over an uneven 16,387-scene sharding"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--config", "C4", "--spawn-check"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["ranks_seen"] == 8 and line["n_gpus"] == 8
+    assert line["scenes_per_rank"] == 2048 and line["gather_even_scenes"] == 16384
+    assert line["gather_uneven_scenes"] == 16387 and line["gather_ok"], line
 
 
 def test_gpus_flag_must_match_launcher_world_size():

@@ -57,10 +57,10 @@ def _worker(rank, world, port, total, G, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total", [(2, 4), (2, 5), (4, 7), (4, 2)])
+@pytest.mark.parametrize("world,total", [(2, 4), (2, 5), (4, 7), (4, 2), (8, 11), (8, 5)])
 def test_shard_and_gather_equals_single_process(world, total):
-    """Equal shards (4 over 2), uneven shards (5 over 2, 7 over 4) and ranks
-    without scenes (2 over 4): the gathered records equal one process's."""
+    """Equal shards (4 over 2), uneven shards (5 over 2, 7 over 4, 11 over 8) and ranks
+    without scenes (2 over 4, 5 over 8): the gathered records equal one process's."""
     G = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
