@@ -37,7 +37,7 @@ extern "C" {
 #define MPCG_NU 2            /* the unicycle models */
 #define MPCG_MAX_NU 3
 #define MPCG_NVAR 7
-#define MPCG_ABI_VERSION 8
+#define MPCG_ABI_VERSION 9
 /* mpcg_problem.model */
 #define MPCG_MODEL_UNICYCLE 0      /* contouring unicycle (+ slack state): MPCBase + Contouring (+ Consistency) */
 #define MPCG_MODEL_BICYCLE_CA 1    /* curvature-aware bicycle: MPCBase(a, w, slack) + CurvatureAwareContouring */
@@ -109,8 +109,9 @@ typedef struct mpcg_problem {
     /* ABI 8: the interior point's profile (mpcg_problem_set_qp_profile sets the group).
      * MPCG_QP_HPIPM (the default of mpcg_problem_from_map*): HPIPM's BALANCE mode as acados configures it,
      * which the reference leaves at acados' defaults but for four options (generate_acados_solver.py:162-173):
-     * qp_mu0 10, qp_thr0 0.1, qp_t_min 1e-16, qp_mu_max 0 and 1 / 1 / 2 / 0 / 1 below.  MPCG_QP_ROBUST:
-     * the round-4 algorithm, qp_mu0 1, qp_thr0 1, qp_t_min 1e-12, qp_mu_max 1e8 and 0 / 0 / 0 / 1 / 0. */
+     * qp_mu0 10, qp_thr0 0.1, qp_t_min 1e-16, qp_mu_max 0 and 1 / 1 / 2 / 0 / 1 below (ABI 9: qp_pivot_zero 1).
+     * MPCG_QP_ROBUST: the round-4 algorithm, qp_mu0 1, qp_thr0 1, qp_t_min 1e-12, qp_mu_max 1e8 and 0 / 0 / 0 /
+     * 1 / 0 (qp_pivot_zero 0). */
     int qp_profile;                /* MPCG_QP_*: what mpcg_problem_set_qp_profile wrote (informative) */
     int qp_init_move;              /* HPIPM init_var at a cold start: a box row whose gap is below qp_thr0 moves
                                       the primal start inside its bounds (to the midpoint when both are) */
@@ -120,6 +121,10 @@ typedef struct mpcg_problem {
                                       residual above max(qp_tol, 1e-3 x the iterate's residual)) */
     int qp_sigma_clip;             /* 1: sigma = min(mu_aff / mu, 1)^3; 0: (mu_aff / mu)^3 (HPIPM) */
     int qp_maxit_first;            /* 1: the iteration cap is tested before convergence (HPIPM's exit order) */
+    /* ABI 9 */
+    int qp_pivot_zero;             /* a non-positive Cholesky pivot of the Riccati recursion: 1 BLASFEO's dpotrf rule
+                                      (zero diagonal and inverse, the column below multiplied by it, the QP goes on;
+                                      MPCG_QP_HPIPM), 0 the QP ends with the NaN status (MPCG_QP_ROBUST) */
 } mpcg_problem;
 
 #define MPCG_QP_HPIPM 0

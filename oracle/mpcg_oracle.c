@@ -546,6 +546,8 @@ typedef struct {
     /* Riccati storage */
     double L[NU][NU], Y[NU][NX], P[NX][NX], p[NX], y[NU];
     double il[NU];  /* reciprocal pivots 1/L_ii (default build, nu 2) */
+    /* square-root Riccati (qp_ric_alg 1): the state block of the stage's Cholesky factor, P = Lx Lx' */
+    double Lx[NX][NX];
     double Hh[NZ][NZ], q[NZ];
     double dz[NZ], ddz[NZ], pi[NX], pin[NX];
     /* iterative refinement (qp_itref_corr_max): the iterate's stationarity residual, the
@@ -558,6 +560,10 @@ typedef struct {
 typedef struct {
     int N;
     qp_stage *st; /* N+1 */
+    /* the Riccati recursion's form and its pivot rule (orc_problem.qp_ric_alg, qp_pivot_zero), and
+     * HPIPM's lq_fact switch: lq_fact 1 -> after an inaccurate Cholesky factorisation (the predictor's
+     * linear residual above 1e-5) the QP's remaining factorisations are LQ ones (force_lq) */
+    int ric_sqrt, pivot_zero, lq_fact, force_lq;
 } qp_ws;
 
 /* stationarity residual of stage k on its free variables */
@@ -697,8 +703,185 @@ static void dyn_res(qp_ws *w, int k, double r[NX]) {
     }
 }
 
+/* BLASFEO dpotrf_l of the leading n x n block of M (row stride NZ) into L, with the inverse diagonal
+ * in il: column j's pivot d = M_jj - sum_m L_jm^2; d > 0: L_jj = sqrt(d), il_j = 1 / L_jj, else (with
+ * pivot_zero) L_jj = il_j = 0 -- the column below is multiplied by il_j, so a non-positive pivot zeroes
+ * its column and the factorisation goes on.  literal: divisions by L_jj instead of the inverse (a zero
+ * pivot then gives a zero column too).  Returns -1 on a non-positive pivot without pivot_zero. */
+static int potrf_l(int n, double (*M)[NZ], double (*L)[NZ], double *il, int pivot_zero) {
+    for (int j = 0; j < n; j++) {
+        double d = M[j][j];
+        for (int m = 0; m < j; m++) d -= L[j][m] * L[j][m];
+        double ljj = 0.0, inv = 0.0;
+        if (d > 0.0) {
+            ljj = sqrt(d);
+            inv = 1.0 / ljj;
+        } else if (!pivot_zero) {
+            return -1;
+        }
+        L[j][j] = ljj;
+        il[j] = inv;
+        for (int i = j + 1; i < n; i++) {
+            double acc = M[i][j];
+            for (int m = 0; m < j; m++) acc -= L[i][m] * L[j][m];
+            L[i][j] = KF ? acc * inv : (ljj != 0.0 ? acc / ljj : 0.0);
+        }
+        for (int i = 0; i < j; i++) L[i][j] = 0.0;
+    }
+    return 0;
+}
+
+static void lq_stage(qp_stage *S, const qp_stage *S1, int terminal, double (*L)[NZ]);
+
+/* Square-root Riccati factorisation (HPIPM square_root_alg 1, which acados selects by default:
+ * acados_template's qp_solver_ric_alg 1 -- restated, version unpinned): the cost-to-go
+ * is carried as its Cholesky factor, P_k = Lx_k Lx_k'.  Per stage, AL = F_k' Lx_{k+1} (BLASFEO
+ * dtrmm_rlnn), M = Hh_k + AL AL' (dsyrk), and one Cholesky of the whole nz x nz block M (dpotrf_l):
+ * its input block gives L and the inverse pivots, its off-diagonal block Y' = Lxu, its state block
+ * Lx_k.  The terminal stage factorises its state block.  With pivot_zero a non-positive pivot -- of the
+ * input or of the state block -- continues with a zero column (BLASFEO); P is also formed (Lx Lx') for
+ * the diagnostics that read it. */
+static int riccati_factor_sqrt(qp_ws *w) {
+    int N = w->N;
+    qp_stage *SN = &w->st[N];
+    {
+        double M[NZ][NZ], L[NZ][NZ], il[NZ];
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++) M[i][j] = SN->Hh[NU + i][NU + j];
+        if (w->force_lq) lq_stage(SN, NULL, 1, L);
+        else if (potrf_l(NX, M, L, il, w->pivot_zero)) return -1;
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++) SN->Lx[i][j] = L[i][j];
+    }
+    for (int k = N - 1; k >= 0; k--) {
+        qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
+        double AL[NZ][NX], M[NZ][NZ], L[NZ][NZ], il[NZ];
+        /* AL = BAbt Lx_{k+1}: BAbt[i][m] = F[m][i], Lx lower triangular */
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NX; j++) {
+                double acc = 0.0;
+                for (int m = j; m < NX; m++) acc += (i < NU ? S->B[m][i] : S->A[m][i - NU]) * S1->Lx[m][j];
+                AL[i][j] = acc;
+            }
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j <= i; j++) {
+                double acc = 0.0;
+                for (int m = 0; m < NX; m++) acc += AL[i][m] * AL[j][m];
+                M[i][j] = S->Hh[i][j] + acc;
+                M[j][i] = M[i][j];
+            }
+        if (w->force_lq) {
+            lq_stage(S, S1, 0, L);
+            for (int i = 0; i < NZ; i++) il[i] = 1.0 / L[i][i];
+        } else if (potrf_l(NZ, M, L, il, w->pivot_zero)) {
+            return -1;
+        }
+        for (int i = 0; i < NU; i++) {
+            for (int j = 0; j < NU; j++) S->L[i][j] = L[i][j];
+            S->il[i] = il[i];
+        }
+        for (int i = 0; i < NU; i++)
+            for (int j = 0; j < NX; j++) S->Y[i][j] = L[NU + j][i];
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++) S->Lx[i][j] = L[NU + i][NU + j];
+    }
+    for (int k = 0; k <= N; k++) {
+        qp_stage *S = &w->st[k];
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++) {
+                double acc = 0.0;
+                for (int m = 0; m <= (i < j ? i : j); m++) acc += S->Lx[i][m] * S->Lx[j][m];
+                S->P[i][j] = acc;
+            }
+    }
+    return 0;
+}
+
+/* Lower-triangular L with positive diagonal and L L' = W W' for the n x m (m >= n) matrix W (row stride
+ * ld): Householder LQ (LAPACK dgelqf's reflections, the diagonal made positive as HPIPM's _pd kernels
+ * return it).  The factor the Cholesky of W W' would give, without forming W W' -- no cancellation, no
+ * failing pivot */
+static void lq_lower(int n, int m, double *W, int ld, double (*L)[NZ]) {
+    for (int i = 0; i < n; i++) {
+        double *wi = W + (size_t)i * ld;
+        double nrm = 0.0;
+        for (int j = i; j < m; j++) nrm += wi[j] * wi[j];
+        nrm = sqrt(nrm);
+        if (nrm > 0.0) {
+            const double alpha = wi[i] > 0.0 ? -nrm : nrm;
+            /* v = w_i[i:] - alpha e_0, H = I - 2 v v' / (v' v); applied to rows i..n-1 from the right */
+            double v[ORC_MAX_NZW];
+            double vv = 0.0;
+            for (int j = i; j < m; j++) { v[j] = wi[j] - (j == i ? alpha : 0.0); vv += v[j] * v[j]; }
+            if (vv > 0.0) {
+                for (int r = i; r < n; r++) {
+                    double *wr = W + (size_t)r * ld;
+                    double dot = 0.0;
+                    for (int j = i; j < m; j++) dot += wr[j] * v[j];
+                    const double f = 2.0 * dot / vv;
+                    for (int j = i; j < m; j++) wr[j] -= f * v[j];
+                }
+            }
+        }
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < NZ; j++) L[i][j] = 0.0;
+    for (int j = 0; j < n; j++) {
+        const double s = W[(size_t)j * ld + j] < 0.0 ? -1.0 : 1.0;  /* positive diagonal: flip column j */
+        for (int i = j; i < n; i++) L[i][j] = s * W[(size_t)i * ld + j];
+    }
+}
+
+/* HPIPM's LQ factorisation of one stage (d_ocp_qp_fact_lq_solve_kkt_step, square-root form): the stage's
+ * factor from the wide matrix [chol(H_k) | sqrt(lam_c / t_c) D_c' for every inequality row | F_k' Lx_{k+1}]
+ * (the Hessian's Cholesky, the barrier of each row, the propagated cost-to-go factor): L L' = M as in the
+ * Cholesky path, computed without forming M.  n = nz (k < N) or nx (stage N, its state block, no rows) */
+static void lq_stage(qp_stage *S, const qp_stage *S1, int terminal, double (*L)[NZ]) {
+    const int n = terminal ? NX : NZ, off = terminal ? NU : 0;
+    double Hs[NZ][NZ], Lh[NZ][NZ], il[NZ];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) Hs[i][j] = S->H[off + i][off + j];
+    potrf_l(n, Hs, Lh, il, 1);
+    const int m = n + (terminal ? 0 : S->ni) + (terminal ? 0 : NX);
+    static __thread double W[NZ * ORC_MAX_NZW];
+    for (int i = 0; i < n; i++) {
+        double *wi = W + (size_t)i * ORC_MAX_NZW;
+        for (int j = 0; j < m; j++) wi[j] = 0.0;
+        for (int j = 0; j <= i; j++) wi[j] = Lh[i][j];
+    }
+    if (!terminal) {
+        for (int c = 0; c < S->ni; c++) {
+            const double sw = sqrt(S->lam[c] * (1.0 / S->t[c]));
+            for (int i = 0; i < NZ; i++) W[(size_t)i * ORC_MAX_NZW + n + c] = S->D[c][i] * sw;
+        }
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NX; j++) {
+                double acc = 0.0;
+                for (int q = j; q < NX; q++) acc += (i < NU ? S->B[q][i] : S->A[q][i - NU]) * S1->Lx[q][j];
+                W[(size_t)i * ORC_MAX_NZW + n + S->ni + j] = acc;
+            }
+    }
+    lq_lower(n, m, W, ORC_MAX_NZW, L);
+}
+
+/* P_{k} v as the square-root form applies it: Lx (Lx' v) (BLASFEO dtrmv_ltn, then dtrmv_lnn) */
+static void lx_apply(const qp_stage *S, const double *v, double *out) {
+    double t[NX];
+    for (int i = 0; i < NX; i++) {
+        double acc = 0.0;
+        for (int m = i; m < NX; m++) acc += S->Lx[m][i] * v[m];
+        t[i] = acc;
+    }
+    for (int i = 0; i < NX; i++) {
+        double acc = 0.0;
+        for (int m = 0; m <= i; m++) acc += S->Lx[i][m] * t[m];
+        out[i] = acc;
+    }
+}
+
 /* Riccati factorisation of the barrier-augmented Hessians Hh. returns 0 ok */
 static int riccati_factor(qp_ws *w) {
+    if (w->ric_sqrt) return riccati_factor_sqrt(w);
     int N = w->N;
     qp_stage *SN = &w->st[N];
     for (int i = 0; i < NX; i++)
@@ -724,14 +907,17 @@ static int riccati_factor(qp_ws *w) {
             /* kernel forms: both reciprocal square roots from the block entries,
              * 1/l11 = l00 / sqrt(m00 m11 - m10^2) */
             const double m00 = M[0][0], m10 = M[1][0], m11 = M[1][1];
-            if (!(m00 > 0.0)) return -1;
-            const double il00 = 1.0 / sqrt(m00);
             const double det = fma(m00, m11, -(m10 * m10));
-            if (!(det > 0.0)) return -1;
-            const double ild = 1.0 / sqrt(det);
-            S->L[0][0] = m00 * il00; S->L[1][0] = m10 * il00; S->L[0][1] = 0.0;
-            S->il[0] = il00; S->il[1] = S->L[0][0] * ild;
-            S->L[1][1] = 1.0 / S->il[1];
+            if (!w->pivot_zero && (!(m00 > 0.0) || !(det > 0.0))) return -1;
+            /* pivot_zero: the kernel's BLASFEO rule -- a non-positive first pivot gives a zero first
+             * column (l10 = 0, the second pivot is then m11 itself); a non-positive second pivot
+             * (det / m00 <= 0) a zero second column */
+            const double il00 = m00 > 0.0 ? 1.0 / sqrt(m00) : 0.0;
+            const double l00 = m00 * il00;
+            const double il11 = m00 > 0.0 ? (det > 0.0 ? l00 * (1.0 / sqrt(det)) : 0.0) : (m11 > 0.0 ? 1.0 / sqrt(m11) : 0.0);
+            S->L[0][0] = l00; S->L[1][0] = m10 * il00; S->L[0][1] = 0.0;
+            S->il[0] = il00; S->il[1] = il11;
+            S->L[1][1] = il11 != 0.0 ? 1.0 / il11 : 0.0;
             for (int j = 0; j < NX; j++) {
                 S->Y[0][j] = M[0][NU + j] * S->il[0];
                 S->Y[1][j] = (M[1][NU + j] - S->L[1][0] * S->Y[0][j]) * S->il[1];
@@ -748,11 +934,20 @@ static int riccati_factor(qp_ws *w) {
         for (int j = 0; j < NU; j++) {
             double d = M[j][j];
             for (int m = 0; m < j; m++) d -= S->L[j][m] * S->L[j][m];
+            if (!(d > 0.0) && w->pivot_zero) {
+                /* BLASFEO dpotrf's non-positive pivot: zero diagonal, zero inverse, the column below
+                 * multiplied by that zero; the factorisation goes on */
+                S->L[j][j] = 0.0;
+                S->il[j] = 0.0;
+                for (int i = j + 1; i < NU; i++) S->L[i][j] = 0.0;
+                for (int i = 0; i < j; i++) S->L[i][j] = 0.0;
+                continue;
+            }
             if (!(d > 0.0)) return -1;
             if (KK) {
                 S->il[j] = 1.0 / sqrt(d);
                 d = d * S->il[j];
-            } else {
+            } else {  /* (a positive pivot here: the non-positive ones took the zero column above) */
                 d = sqrt(d);
                 S->il[j] = 1.0 / d;
             }
@@ -769,7 +964,7 @@ static int riccati_factor(qp_ws *w) {
             for (int i = 0; i < NU; i++) {
                 double acc = M[i][NU + j];
                 for (int m = 0; m < i; m++) acc -= S->L[i][m] * S->Y[m][j];
-                S->Y[i][j] = KF ? acc * S->il[i] : acc / S->L[i][i];
+                S->Y[i][j] = KF ? acc * S->il[i] : (S->L[i][i] != 0.0 ? acc / S->L[i][i] : 0.0);
             }
         for (int i = 0; i < NX; i++)
             for (int j = 0; j < NX; j++) {
@@ -799,10 +994,17 @@ static void riccati_solve_r(qp_ws *w, double (*r)[NX]) {
     for (int k = N - 1; k >= 0; k--) {
         qp_stage *S = &w->st[k], *S1 = &w->st[k + 1];
         double v[NX], m[NZ];
-        for (int i = 0; i < NX; i++) {
-            double acc = S1->p[i];
-            for (int j = 0; j < NX; j++) acc += S1->P[i][j] * r[k][j];
-            v[i] = acc;
+        if (w->ric_sqrt) {
+            /* HPIPM (square root): Lx (Lx' b) + p */
+            double Pb[NX];
+            lx_apply(S1, r[k], Pb);
+            for (int i = 0; i < NX; i++) v[i] = Pb[i] + S1->p[i];
+        } else {
+            for (int i = 0; i < NX; i++) {
+                double acc = S1->p[i];
+                for (int j = 0; j < NX; j++) acc += S1->P[i][j] * r[k][j];
+                v[i] = acc;
+            }
         }
         for (int i = 0; i < NZ; i++) {
             double acc = S->q[i];
@@ -812,7 +1014,7 @@ static void riccati_solve_r(qp_ws *w, double (*r)[NX]) {
         for (int i = 0; i < NU; i++) { /* y = L^{-1} m_u */
             double acc = m[i];
             for (int q = 0; q < i; q++) acc -= S->L[i][q] * S->y[q];
-            S->y[i] = KF ? acc * S->il[i] : acc / S->L[i][i];
+            S->y[i] = KF ? acc * S->il[i] : (S->L[i][i] != 0.0 ? acc / S->L[i][i] : 0.0);
         }
         for (int i = 0; i < NX; i++) {
             double acc = m[NU + i];
@@ -833,7 +1035,7 @@ static void riccati_solve_r(qp_ws *w, double (*r)[NX]) {
         for (int i = NU - 1; i >= 0; i--) { /* L' du = -c */
             double acc = -c[i];
             for (int q = i + 1; q < NU; q++) acc -= S->L[q][i] * du[q];
-            du[i] = KF ? acc * S->il[i] : acc / S->L[i][i];
+            du[i] = KF ? acc * S->il[i] : (S->L[i][i] != 0.0 ? acc / S->L[i][i] : 0.0);
         }
         for (int i = 0; i < NU; i++) S->ddz[i] = du[i];
         for (int i = 0; i < NX; i++) S->ddz[NU + i] = (k == 0) ? 0.0 : dx[i];
@@ -844,10 +1046,16 @@ static void riccati_solve_r(qp_ws *w, double (*r)[NX]) {
             for (int j = 0; j < NX; j++) acc += S->A[i][j] * dx[j];
             dxn[i] = acc;
         }
-        for (int i = 0; i < NX; i++) {
-            double acc = S1->p[i];
-            for (int j = 0; j < NX; j++) acc += S1->P[i][j] * dxn[j];
-            S->pin[i] = acc;
+        if (w->ric_sqrt) {
+            double Pd[NX];
+            lx_apply(S1, dxn, Pd);
+            for (int i = 0; i < NX; i++) S->pin[i] = Pd[i] + S1->p[i];
+        } else {
+            for (int i = 0; i < NX; i++) {
+                double acc = S1->p[i];
+                for (int j = 0; j < NX; j++) acc += S1->P[i][j] * dxn[j];
+                S->pin[i] = acc;
+            }
         }
         memcpy(dx, dxn, sizeof dx);
     }
@@ -960,8 +1168,10 @@ static void lin_residuals(qp_ws *w, double res[4]) {
     }
 }
 
-static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm, int *n_center, int *n_itref) {
+static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm, int *n_center, int *n_itref,
+                    int *n_lq) {
     int N = w->N;
+    w->force_lq = w->lq_fact == 2;  /* HPIPM lq_fact 2: LQ factorisations only */
     if (!warm) {
         /* cold start (HPIPM init_var, warm_start 0): ux = 0, pi = 0; then per row t = gap at
          * ux clipped below at thr0, lambda = mu0 / t.  With qp_init_move (HPIPM's own start), the
@@ -1074,6 +1284,21 @@ static int qp_solve(const orc_problem *pr, qp_ws *w, int *iters, int warm, int *
         build_q(w);
         riccati_solve(w);
         ineq_steps(w, NULL);
+        if (w->lq_fact == 1 && !w->force_lq) {
+            /* HPIPM lq_fact 1: the predictor direction's linear KKT residual; above 1e-5 in any component
+             * (or NaN) the Cholesky factorisation was inaccurate, and this and every later factorisation of
+             * the QP is an LQ one; the predictor is solved again with it */
+            double lr[4];
+            lin_residuals(w, lr);
+            if (!(lr[0] <= 1e-5) || !(lr[1] <= 1e-5) || !(lr[2] <= 1e-5) || !(lr[3] <= 1e-5)) {
+                w->force_lq = 1;
+                ++*n_lq;
+                riccati_factor(w);
+                build_q(w);
+                riccati_solve(w);
+                ineq_steps(w, NULL);
+            }
+        }
         double aa = max_step(w);
         if (aa > 1.0) aa = 1.0;
         double comp_aff = 0.0;
@@ -1346,6 +1571,11 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
 
     qp_ws w;
     w.N = N;
+    /* the square-root Riccati of HPIPM's profile in the kernel-agnostic builds (the kernel-forms build
+     * mirrors the kernel, which runs the classical form) */
+    w.ric_sqrt = pr->qp_ric_alg == 1 && !KK;
+    w.pivot_zero = pr->qp_pivot_zero != 0;
+    w.lq_fact = w.ric_sqrt ? pr->qp_lq_fact : 0;
     w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
     size_t nrow = (size_t)(N + 1) * maxi;
     double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));
@@ -1400,7 +1630,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
 
     double *hh = (double *)malloc(sizeof(double) * nh * NZ * NZ);
     int acados_status = AC_SUCCESS, qp_status = AC_SUCCESS, sqp_iter = 0, qp_iter_total = 0, n_maxit = 0;
-    int n_center = 0, n_itref = 0;
+    int n_center = 0, n_itref = 0, n_lq = 0;
     double res_eq = 0.0;
 
     const int sqp_mode = pr->nlp_solver == 1;
@@ -1441,7 +1671,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
          * the first with warm_start_first_qp) */
         int qit = 0;
         const int warm = have_qp && pr->qp_warm_start == 2 && ((sqp_mode && it > 0) || pr->qp_warm_first);
-        qp_status = qp_solve(pr, &w, &qit, warm, &n_center, &n_itref);
+        qp_status = qp_solve(pr, &w, &qit, warm, &n_center, &n_itref, &n_lq);
         have_qp = 1;
         qp_iter_total += qit;
         sqp_iter++;
@@ -1513,6 +1743,7 @@ int orc_solve_full(const orc_problem *pr, const double *params, const double *wa
         info->qp_maxiter = n_maxit;
         info->qp_center = n_center;
         info->qp_itref = n_itref;
+        info->qp_lq = n_lq;
     }
     free(hh); free(lamh); free(pi); free(z);
     free(ibl); free(dbl); free(Dall); free(w.st);
@@ -1593,6 +1824,11 @@ int orc_qp_data(const orc_problem *pr, const double *params, const double *warm,
     orc_h_bounds(pr, lh, uh);
     qp_ws w;
     w.N = N;
+    /* the square-root Riccati of HPIPM's profile in the kernel-agnostic builds (the kernel-forms build
+     * mirrors the kernel, which runs the classical form) */
+    w.ric_sqrt = pr->qp_ric_alg == 1 && !KK;
+    w.pivot_zero = pr->qp_pivot_zero != 0;
+    w.lq_fact = w.ric_sqrt ? pr->qp_lq_fact : 0;
     w.st = (qp_stage *)calloc(N + 1, sizeof(qp_stage));
     size_t nrow = (size_t)(N + 1) * maxi;
     double (*Dall)[NZ] = (double (*)[NZ])calloc(nrow, sizeof(double[NZ]));

@@ -38,9 +38,11 @@ ORC_MAX_NU, ORC_MAX_NX = 3, 6
 # generate_acados_solver.py:162-173), "robust" is round 4's algorithm.
 QP_PROFILES = {
     "hpipm": dict(qp_mu0=10.0, qp_thr0=0.1, qp_t_min=1e-16, qp_mu_max=0.0, qp_init_move=1, qp_cond_pred_corr=1,
-                  qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1),
+                  qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1, qp_ric_alg=1, qp_pivot_zero=1,
+                  qp_lq_fact=0),
     "robust": dict(qp_mu0=1.0, qp_thr0=1.0, qp_t_min=1e-12, qp_mu_max=1e8, qp_init_move=0, qp_cond_pred_corr=0,
-                   qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0),
+                   qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0, qp_ric_alg=0, qp_pivot_zero=0,
+                   qp_lq_fact=0),
 }
 
 
@@ -68,6 +70,7 @@ class OrcProblem(C.Structure):
         ("qp_t_min", C.c_double), ("qp_mu_max", C.c_double),
         ("qp_init_move", C.c_int), ("qp_cond_pred_corr", C.c_int), ("qp_itref_corr_max", C.c_int),
         ("qp_sigma_clip", C.c_int), ("qp_maxit_first", C.c_int),
+        ("qp_ric_alg", C.c_int), ("qp_pivot_zero", C.c_int), ("qp_lq_fact", C.c_int),
     ]
 
 
@@ -75,7 +78,7 @@ class OrcInfo(C.Structure):
     _fields_ = [("sqp_iter", C.c_int), ("qp_iter_total", C.c_int), ("qp_status", C.c_int),
                 ("res_eq", C.c_double), ("pobj", C.c_double),
                 ("res_stat", C.c_double), ("res_ineq", C.c_double), ("res_comp", C.c_double),
-                ("qp_maxiter", C.c_int), ("qp_center", C.c_int), ("qp_itref", C.c_int)]
+                ("qp_maxiter", C.c_int), ("qp_center", C.c_int), ("qp_itref", C.c_int), ("qp_lq", C.c_int)]
 
 
 def build(force: bool = False) -> str:
@@ -167,7 +170,7 @@ def problem_from_layout(layout, **opts) -> OrcProblem:
     # floor of t and lambda after every interior-point step, the divergence test (<= 0: none) and
     # the structural switches of the profile
     for f in ("qp_t_min", "qp_mu_max", "qp_init_move", "qp_cond_pred_corr", "qp_itref_corr_max", "qp_sigma_clip",
-              "qp_maxit_first"):
+              "qp_maxit_first", "qp_ric_alg", "qp_pivot_zero", "qp_lq_fact"):
         setattr(pr, f, opts.get(f, prof[f]))
     return pr
 
@@ -315,7 +318,7 @@ class Oracle:
                    res_eq=get("res_eq", float), res_stat=get("res_stat", float),
                    res_ineq=get("res_ineq", float), res_comp=get("res_comp", float),
                    qp_maxiter=get("qp_maxiter", np.int32), qp_center=get("qp_center", np.int32),
-                   qp_itref=get("qp_itref", np.int32))
+                   qp_itref=get("qp_itref", np.int32), qp_lq=get("qp_lq", np.int32))
         if return_lam:
             out["lam"] = lo
         if return_qp:

@@ -443,6 +443,8 @@ int mpcg_problem_set_qp_profile(mpcg_problem* pr, int profile) {
     pr->qp_itref_corr_max = h ? 2 : 0;
     pr->qp_sigma_clip = !h;
     pr->qp_maxit_first = h;
+    // BLASFEO's dpotrf continues past a non-positive pivot with a zero inverse (ABI 9)
+    pr->qp_pivot_zero = h;
     return 0;
 }
 

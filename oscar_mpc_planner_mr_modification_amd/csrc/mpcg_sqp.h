@@ -658,16 +658,16 @@ __host__ __device__ inline bool needs_full(const mpcg_problem& pr) {
 // The interior point's profile (mpcg_problem_set_qp_profile) as a template parameter of
 // the kernel: the lean kernels are compiled once per profile with its structural switches (the primal box
 // move, the conditional corrector, the corrector's refinement, sigma's clip, the exit order, the divergence
-// test) as constants, so neither profile carries the other's code or its live state.  PROF_RUNTIME reads
+// test, the pivot rule) as constants, so neither profile carries the other's code or its live state.  PROF_RUNTIME reads
 // them from mpcg_problem (the FULL variant, and a lean call with a combination of switches that is neither
 // profile).  The continuous constants (mu0, thr0, t_min, mu_max) stay run-time arguments.
 enum { PROF_RUNTIME = 0, PROF_HPIPM = 1, PROF_ROBUST = 2 };
 __host__ __device__ inline int qp_profile_kind(const mpcg_problem& pr) {
     if (pr.qp_init_move == 1 && pr.qp_cond_pred_corr == 1 && pr.qp_itref_corr_max == 2 && pr.qp_sigma_clip == 0 &&
-        pr.qp_maxit_first == 1 && !(pr.qp_mu_max > 0.0))
+        pr.qp_maxit_first == 1 && !(pr.qp_mu_max > 0.0) && pr.qp_pivot_zero == 1)
         return PROF_HPIPM;
     if (pr.qp_init_move == 0 && pr.qp_cond_pred_corr == 0 && pr.qp_itref_corr_max == 0 && pr.qp_sigma_clip == 1 &&
-        pr.qp_maxit_first == 0 && pr.qp_mu_max > 0.0)
+        pr.qp_maxit_first == 0 && pr.qp_mu_max > 0.0 && pr.qp_pivot_zero == 0)
         return PROF_ROBUST;
     return PROF_RUNTIME;
 }

@@ -44,6 +44,8 @@ class MpcgProblem(C.Structure):
         # ABI 8: the interior point's profile
         ("qp_profile", C.c_int), ("qp_init_move", C.c_int), ("qp_cond_pred_corr", C.c_int),
         ("qp_itref_corr_max", C.c_int), ("qp_sigma_clip", C.c_int), ("qp_maxit_first", C.c_int),
+        # ABI 9: BLASFEO's rule for a non-positive Cholesky pivot
+        ("qp_pivot_zero", C.c_int),
     ]
 
 
@@ -60,12 +62,12 @@ DEFAULT_OPTIONS = dict(qp_tol=1e-5, qp_iter_max=50, reg_eps=1e-4, res_eq_fail=1e
 # "robust" is round 4's interior point.  Any field can be overridden by name.
 QP_PROFILES = {
     "hpipm": dict(qp_profile_id=0, qp_mu0=10.0, qp_thr0=0.1, qp_t_min=1e-16, qp_mu_max=0.0, qp_init_move=1,
-                  qp_cond_pred_corr=1, qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1),
+                  qp_cond_pred_corr=1, qp_itref_corr_max=2, qp_sigma_clip=0, qp_maxit_first=1, qp_pivot_zero=1),
     "robust": dict(qp_profile_id=1, qp_mu0=1.0, qp_thr0=1.0, qp_t_min=1e-12, qp_mu_max=1e8, qp_init_move=0,
-                   qp_cond_pred_corr=0, qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0),
+                   qp_cond_pred_corr=0, qp_itref_corr_max=0, qp_sigma_clip=1, qp_maxit_first=0, qp_pivot_zero=0),
 }
 QP_FIELDS = ("qp_mu0", "qp_thr0", "qp_t_min", "qp_mu_max", "qp_init_move", "qp_cond_pred_corr", "qp_itref_corr_max",
-             "qp_sigma_clip", "qp_maxit_first")
+             "qp_sigma_clip", "qp_maxit_first", "qp_pivot_zero")
 NLP_SOLVER = {"SQP_RTI": 0, "SQP": 1}
 # ContouringSecondOrderUnicycleModel bounds (solver_model.py:204-205), z = [a, w, x, y, psi, v, s]
 UNICYCLE_LB = (-2.0, -0.8, -2000.0, -2000.0, -4 * np.pi, -0.01, -1.0)
@@ -152,7 +154,7 @@ class MpcgScenarioIo(C.Structure):
                 ("deceleration", C.c_double)]
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 EXPORTS = ("mpcg_abi_version", "mpcg_last_error", "mpcg_supported", "mpcg_num_h", "mpcg_lam_size", "mpcg_qp_mem_size",
            "mpcg_problem_from_map", "mpcg_problem_from_map_model", "mpcg_solve", "mpcg_context_create", "mpcg_context_destroy",
            "mpcg_context_solve", "mpcg_context_set_iterations", "mpcg_solve_batch_device", "mpcg_solve_batch_host", "mpcg_select_best_device", "mpcg_prepare", "mpcg_advance",

@@ -51,7 +51,7 @@ def test_host_only_queries(lib):
     from oscar_mpc_planner_mr_modification_amd.layouts import config_layout
     from oscar_mpc_planner_mr_modification_amd.native_spec import problem_from_layout
     lib.mpcg_abi_version.restype = C.c_int
-    assert lib.mpcg_abi_version() == 8
+    assert lib.mpcg_abi_version() == 9
     for cfg in ("C1", "C2", "C3", "C4", "C5"):
         pr = problem_from_layout(config_layout(cfg))
         assert lib.mpcg_supported(C.byref(pr)) == 0, cfg
