@@ -69,7 +69,10 @@ def _load():
     lib.mpcg_select_lowest_cost_device.restype = C.c_int
     lib.mpcg_winner_records_device.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
     lib.mpcg_winner_records_device.restype = C.c_int
-    if lib.mpcg_abi_version() != ABI_VERSION:
+    # (MPCG_ABI_ACCEPT_OLDER, A/B timing runs of an earlier round's library only: ABI versions whose
+    # mpcg_problem is a prefix of this one -- later ABIs only append fields)
+    older = {int(v) for v in os.environ.get("MPCG_ABI_ACCEPT_OLDER", "").split(",") if v.strip().isdigit()}
+    if lib.mpcg_abi_version() != ABI_VERSION and lib.mpcg_abi_version() not in {v for v in older if 8 <= v < ABI_VERSION}:
         raise ImportError(f"{LIB_PATH}: ABI {lib.mpcg_abi_version()} != {ABI_VERSION}; rebuild")
     return lib
 

@@ -42,7 +42,8 @@ def main():
     for rep in range(args.reps):
         for cfg in args.configs.split(","):
             for name in args.run.split(","):
-                env = dict(os.environ, MPCG_LIB=lib(name))
+                # (an earlier round's library, ABI 8: its mpcg_problem is a prefix of ABI 9's)
+                env = dict(os.environ, MPCG_LIB=lib(name), MPCG_ABI_ACCEPT_OLDER="8")
                 r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--no-cpu",
                                     "--steps", str(args.steps), "--warmup", "2"], env=env, capture_output=True,
                                    text=True, timeout=600)

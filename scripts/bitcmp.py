@@ -47,7 +47,7 @@ def main():
         for i, lib in enumerate(libs):
             f = os.path.join(tmp, f"{cfg}_{i}.npz")
             subprocess.run([sys.executable, os.path.abspath(__file__), "--child", cfg, a.profile, f],
-                           env=dict(os.environ, MPCG_LIB=lib), check=True)
+                           env=dict(os.environ, MPCG_LIB=lib, MPCG_ABI_ACCEPT_OLDER="8"), check=True)
             outs.append(np.load(f))
         ref = outs[0]
         for lib, o in zip(libs[1:], outs[1:]):

@@ -206,17 +206,22 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
                        "sensitive": pert[i]["sensitive"] or po["sensitive"]}
     sens = np.zeros(len(same), bool)
     like_run = np.zeros(len(same), bool)
+    exit_run = np.zeros(len(same), bool)
     near = {}
     for i, po in pert.items():
         sens[i] = po["sensitive"]
         exit_like = int(got["exit"][i]) in set(po["exits"]) | {int(ref["status"][i]), int(lit["status"][i])}
+        exit_run[i] = exit_like
         if got["exit"][i] == 1:
             # within 1e-4 of a successful run; where the runs themselves scatter continuously (a QP
             # stopped at the iteration cap ends wherever its interior point stood: C5B copy 299 on the
             # robust profile), inside the envelope of the runs (+- 1e-4)
             d, which = _nearest_run(got["xtraj"][i], ref, lit, i, po)
             env = _envelope_excess(got["xtraj"][i], ref, lit, i, po)
-            near[i] = (d, which, env)
+            # (and, reported: is the GPU no farther from the default build than the runs themselves are)
+            runs_r = max([float(np.abs(x - ref["xtraj"][i]).max()) for _, x in _successful_runs(ref, lit, i, po)]
+                         or [0.0])
+            near[i] = (d, which, env, float(dx[i]) <= runs_r + 1e-4, runs_r)
             like_run[i] = exit_like and (d <= 1e-4 or env <= 1e-4)
         else:
             # a failed solve's trajectory is wherever the failure left it: its exit code is the outcome
@@ -289,6 +294,9 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
                                          "gpu_dx_nearest_run": near[int(i)][0] if int(i) in near else None,
                                          "nearest_run": near[int(i)][1] if int(i) in near else None,
                                          "gpu_outside_runs_envelope": near[int(i)][2] if int(i) in near else None,
+                                         "runs_radius": near[int(i)][4] if int(i) in near else None,
+                                         "gpu_within_runs_radius": near[int(i)][3] if int(i) in near else None,
+                                         "gpu_exit_like_a_run": bool(exit_run[i]),
                                          "gpu_ends_like_a_run": bool(like_run[i])}
                                         for i in np.flatnonzero(parted & rdec)[:40]],
             "n_parted_rounding_decided": int((parted & rdec).sum()),
@@ -302,6 +310,10 @@ def compare(cfg, S, ws, first=0, warm_first=None, literal=False, solver_type="SQ
             "n_gpu_inside_runs_envelope_only": int(sum(near[i][0] > 1e-4 and near[i][2] <= 1e-4 for i in near
                                                        if parted[i] and rdec[i])),
             "gpu_dx_nearest_run_max": max((near[i][0] for i in near if parted[i] and rdec[i]), default=None),
+            # the weakest form, reported for the robust profile's capped final QPs: the GPU no
+            # farther from the default build than the farthest successful oracle run
+            "gpu_within_runs_radius": bool(all(near[i][0] <= 1e-4 or near[i][2] <= 1e-4 or near[i][3] for i in near
+                                               if parted[i] and rdec[i])),
             "n_unexplained": int(unexplained.sum()),
             "unexplained": [{"i": int(i), "gpu": int(got["exit"][i]), "oracle": int(ref["status"][i]),
                              "gpu_info": got["info"][i].tolist(), "oracle_qp_iter": int(ref["qp_iter"][i]),
