@@ -408,6 +408,22 @@ __host__ __device__ constexpr size_t ws_doubles() {
 #define STAMP_STORE(ptr, sol) do {} while (0)
 #endif
 
+// Unrolling of the stage loops of the interior point: the Riccati recursion (MPCG_UNROLL_FAC) and the split
+// vector chains (MPCG_UNROLL_CHAIN).  Default: fully unrolled (every stage's addresses, lane masks and
+// readlane lanes literal).  MPCG_FAC_UNROLL / MPCG_CHAIN_UNROLL = n: unrolled by n (1: a rolled loop with
+// run-time stage offsets), for A/B runs of the instruction footprint.
+#define MPCG_PRAGMA_(x) _Pragma(#x)
+#ifdef MPCG_FAC_UNROLL
+#define MPCG_UNROLL_FAC MPCG_PRAGMA_(unroll MPCG_FAC_UNROLL)
+#else
+#define MPCG_UNROLL_FAC MPCG_PRAGMA_(unroll)
+#endif
+#ifdef MPCG_CHAIN_UNROLL
+#define MPCG_UNROLL_CHAIN MPCG_PRAGMA_(unroll MPCG_CHAIN_UNROLL)
+#else
+#define MPCG_UNROLL_CHAIN MPCG_PRAGMA_(unroll)
+#endif
+
 // One wavefront per workgroup (blockDim 64): the lanes exchange data through LDS,
 // and a wave's LDS instructions execute in issue order, so an exchange needs a
 // compiler barrier only, not an s_waitcnt on the producing stores before the

@@ -38,22 +38,27 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _assert_parity(r, robust=False):
+# solves known to end away from every oracle run (config, profile, solver type) -> indices; see _assert_parity
+KNOWN_OUTSIDE_RUNS = {("C5B", "robust", "SQP_RTI"): {299}}
+
+
+def _assert_parity(r):
     # every solve on which the GPU parts from the default build is rounding-decided by evidence
     assert r["n_unexplained"] == 0, r["unexplained"]
     # ... and there the GPU ends like one of the oracle runs: an exit code one of them produced and,
     # when successful, a trajectory within 1e-4 of a successful run (default, literal or perturbed) or,
     # where those runs scatter continuously (a QP stopped at the cap), inside their envelope +- 1e-4
-    if robust:
-        # the robust profile (round 4's interior point, not the product's): its one such solve, C5B copy
-        # 299, ends on a QP stopped at the cap whose one-ulp oracle runs scatter by 0.44; the GPU lies 1.9e-3
-        # outside their envelope, at 0.4433 from the default build against the runs' 0.4420 (DESIGN.md §2.3,
-        # profiles/r06g_fullsize_parity_robust.jsonl): held to the runs' radius only
-        assert r["gpu_within_runs_radius"], r["parted_rounding_decided"]
-        assert all(p["gpu_exit_like_a_run"] for p in r["parted_rounding_decided"]), r["parted_rounding_decided"]
-    else:
-        assert r["gpu_near_a_run"], r["parted_rounding_decided"]
-        assert r["parted_rounding_decided_end_like_a_run"], r["parted_rounding_decided"]
+    # The one known exception, on the robust profile (round 4's interior point, not the product's): C5B copy
+    # 299 ends on a QP stopped at the iteration cap, whose 528 one-ulp oracle runs scatter over 0.44; the GPU's
+    # successful trajectory is 0.4433 from the default build against the runs' 0.4420, 1.9e-3 from the nearest
+    # run and outside their envelope by as much (profiles/r06g_fullsize_parity_robust.jsonl).
+    # It is named here so that any other solve that ends away from every oracle run fails the test.
+    known = KNOWN_OUTSIDE_RUNS.get((r["config"], r["qp_profile"], r["solver_type"]), set())
+    outside = {p["i"] for p in r["parted_rounding_decided"] if p["gpu"] == 1 and not p["gpu_ends_like_a_run"]}
+    assert outside <= known, (outside - known, r["parted_rounding_decided"])
+    assert all(p["gpu_exit_like_a_run"] for p in r["parted_rounding_decided"]), r["parted_rounding_decided"]
+    assert all(p["gpu_ends_like_a_run"] for p in r["parted_rounding_decided"] if p["i"] not in known), \
+        r["parted_rounding_decided"]
     # ... and such solves stay rare
     assert r["n_parted_rounding_decided"] <= 0.005 * r["solves"], r["parted_rounding_decided"]
 
@@ -69,7 +74,7 @@ def test_fullsize_parity(cfg, profile):
     print({k: v for k, v in r.items() if k not in ("rounding_decided", "parted_rounding_decided")})
     # the kernel the bench times
     assert r["gpu_variant"] == "lean"
-    _assert_parity(r, robust=profile == "robust")
+    _assert_parity(r)
     # the FULL variant ends every solve like the lean one
     assert r["lean_full_exit_equal"] and r["lean_full_info_equal"], r
     assert r["lean_full_max_abs_dx"] <= 1e-9, r["lean_full_max_abs_dx"]
