@@ -44,7 +44,7 @@ namespace mpcg {
 // grid of a work-queue launch: the workgroups the stream's device holds at once (occupancy x
 // CUs), at most one per problem; cached per device.  MPCG_QUEUE_GRID_PER_CU (A/B only) sets the
 // workgroups per CU.
-template <class C, bool FULL, int PROF>
+template <class C, bool FULL, int PROF, int MODE = MODE_FUSED>
 int queue_grid(int batch, hipStream_t stream) {
     constexpr int MAXDEV = 64;
     static std::atomic<int> resident[MAXDEV];  // 0: not yet asked, -1: no answer
@@ -61,7 +61,7 @@ int queue_grid(int batch, hipStream_t stream) {
 #else
             int cur = 0;
             const bool sw = hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL, PROF>, 64, 0) != hipSuccess)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sqp_kernel<C, FULL, PROF, MODE>, 64, 0) != hipSuccess)
                 per_cu = 0;
             if (sw) (void)hipSetDevice(cur);
 #endif
@@ -73,11 +73,44 @@ int queue_grid(int batch, hipStream_t stream) {
     return r > 0 && r < batch ? r : batch;
 }
 
-template <class C, bool FULL, int PROF>
+template <class C, bool FULL, int PROF, int MODE = MODE_FUSED>
 void launch_kernel(const mpcg_problem* pr, int batch, const mpcg_io* io, hipStream_t st, unsigned long long* stamps,
-                   double* gws, unsigned* queue) {
-    hipLaunchKernelGGL((sqp_kernel<C, FULL, PROF>), dim3(queue ? queue_grid<C, FULL, PROF>(batch, st) : batch),
-                       dim3(64), 0, st, *pr, batch, *io, stamps, gws, queue);
+                   double* gws, unsigned* queue, int split_it = 0) {
+    hipLaunchKernelGGL((sqp_kernel<C, FULL, PROF, MODE>), dim3(queue ? queue_grid<C, FULL, PROF, MODE>(batch, st) : batch),
+                       dim3(64), 0, st, *pr, batch, *io, stamps, gws, queue, split_it);
+}
+
+// the split launch (split_on, MPCG_SPLIT): per RTI iteration a linearisation launch, then an interior-point
+// launch, each zeroing its queue words first when it takes the work queue
+template <class C, int PROF>
+int launch_split(const mpcg_problem* pr, int batch, const mpcg_io* io, hipStream_t st, unsigned long long* stamps,
+                 double* gws, unsigned* qw) {
+#ifdef MPCG_SPLIT_WORDS
+    // (diagnostic: one memset, a queue word of its own per launch)
+    if (hipMemsetAsync(qw, 0, MPCG_QUEUE_BYTES, st) != hipSuccess) return (int)hipGetLastError();
+#endif
+    for (int it = 0; it < pr->sqp_iters; ++it) {
+#ifdef MPCG_SPLIT_WORDS
+        unsigned* ql = kernel_queue<C, MODE_LIN>() ? qw + (2 * it) % 64 : nullptr;
+        unsigned* qq = kernel_queue<C, MODE_QP>() ? qw + (2 * it + 1) % 64 : nullptr;
+#else
+        unsigned* ql = kernel_queue<C, MODE_LIN>() ? qw : nullptr;
+        unsigned* qq = kernel_queue<C, MODE_QP>() ? qw : nullptr;
+        if (ql && hipMemsetAsync(ql, 0, MPCG_QUEUE_BYTES, st) != hipSuccess) return (int)hipGetLastError();
+#endif
+        launch_kernel<C, false, PROF, MODE_LIN>(pr, batch, io, st, stamps, gws, ql, it);
+#ifdef MPCG_SPLIT_SYNC
+        (void)hipStreamSynchronize(st);
+#endif
+#ifndef MPCG_SPLIT_WORDS
+        if (qq && hipMemsetAsync(qq, 0, MPCG_QUEUE_BYTES, st) != hipSuccess) return (int)hipGetLastError();
+#endif
+        launch_kernel<C, false, PROF, MODE_QP>(pr, batch, io, st, stamps, gws, qq, it);
+#ifdef MPCG_SPLIT_SYNC
+        (void)hipStreamSynchronize(st);
+#endif
+    }
+    return (int)hipGetLastError();
 }
 
 template <class C>
@@ -88,7 +121,8 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
     // is read: the GFH stage blocks, and the refinement scratch when the profile refines
     // (qp_itref_corr_max > 0, HPIPM's profile); a robust-profile call of an instance without GFH may
     // pass NULL (one workgroup per problem then, without the work queue)
-    if ((gfh_doubles<C>() > 0 || (pr->qp_itref_corr_max > 0 && itref_doubles<C>() > 0)) && !workspace)
+    if ((gfh_doubles<C>() > 0 || split_on<C>() || (pr->qp_itref_corr_max > 0 && itref_doubles<C>() > 0)) &&
+        !workspace)
         return (int)hipErrorInvalidValue;
     unsigned* queue = C::QUEUE && workspace ? (unsigned*)workspace : nullptr;
     double* gws = workspace ? (double*)((char*)workspace + MPCG_QUEUE_BYTES) : nullptr;
@@ -101,7 +135,15 @@ int launch_instance(const mpcg_problem* pr, int batch, const mpcg_io* io, void* 
     // call whose switches match neither profile on the full variant's run-time switches (without QP
     // memory, residuals or warm start the full variant runs the lean variant's operations)
     const int prof = qp_profile_kind(*pr);
-    if (io->stats || io->qp_in || io->qp_out || needs_full(*pr) || prof == PROF_RUNTIME)
+    const bool full = io->stats || io->qp_in || io->qp_out || needs_full(*pr) || prof == PROF_RUNTIME;
+    if constexpr (split_on<C>()) {
+        if (!full && pr->sqp_iters > 0) {
+            unsigned* qw = (unsigned*)workspace;
+            return prof == PROF_HPIPM ? launch_split<C, PROF_HPIPM>(pr, batch, io, st, stamps, gws, qw)
+                                      : launch_split<C, PROF_ROBUST>(pr, batch, io, st, stamps, gws, qw);
+        }
+    }
+    if (full)
         launch_kernel<C, true, PROF_RUNTIME>(pr, batch, io, st, stamps, gws, queue);
     else if (prof == PROF_HPIPM)
         launch_kernel<C, false, PROF_HPIPM>(pr, batch, io, st, stamps, gws, queue);

@@ -376,10 +376,36 @@ template <class C>
 __host__ __device__ constexpr size_t itref_doubles() {
     return 2 * (size_t)(C::N + 1) * C::NZ + (size_t)C::N * C::NX;
 }
-// one solve's global workspace: the GFH blocks, then the refinement scratch
+// The split launch (MPCG_SPLIT): the lean SQP-RTI as one linearisation
+// kernel and one interior-point kernel per RTI iteration instead of the fused loop, each compiled for
+// its phase alone.  Bit 0: split every lean instance; bit 1: the interior-point launches take the work
+// queue; bit 2: the linearisation launches do.  (A/B build only.)
+#ifndef MPCG_SPLIT
+#define MPCG_SPLIT 0
+#endif
+enum { MODE_FUSED = 0, MODE_LIN = 1, MODE_QP = 2 };
+template <class C>
+__host__ __device__ constexpr bool split_on() {
+    return (MPCG_SPLIT & 1) != 0;
+}
+// the block one split launch hands the next for a solve (global, after the refinement scratch): the
+// iterate (z, pi), the linearisation (g, b, the h rows' gradients, gaps and offsets; [B A] and H unless
+// GFH keeps them in the workspace already), the rows' NLP multipliers lane-major, and the counters
+template <class C>
+struct Carry {
+    using L = LdsOf<C>;
+    static constexpr size_t Z = 0, PI = Z + sizeof(L::z) / 8, G = PI + sizeof(L::pi_nlp) / 8,
+                            B = G + sizeof(L::g) / 8, DG = B + sizeof(L::b) / 8, HD = DG + sizeof(L::Dg) / 8,
+                            DISC = HD + sizeof(L::hd) / 8, H = DISC + sizeof(L::disc) / 8,
+                            F = H + (lds_gfh<C>() ? 0 : sizeof(L::H) / 8),
+                            NLAM = F + (lds_gfh<C>() ? 0 : sizeof(L::F) / 8), META = NLAM + 64 * (size_t)C::HS,
+                            SIZE = META + 8;
+    // META: res_eq, done, acados_status, qp_status, sqp_iter, qp_total, n_maxit
+};
+// one solve's global workspace: the GFH blocks, then the refinement scratch (then the split's carry)
 template <class C>
 __host__ __device__ constexpr size_t ws_doubles() {
-    return gfh_doubles<C>() + itref_doubles<C>();
+    return gfh_doubles<C>() + itref_doubles<C>() + (split_on<C>() ? Carry<C>::SIZE : 0);
 }
 
 // Diagnostic per-phase cycle stamps (separate build with -DMPCG_STAMPS; the
@@ -702,10 +728,10 @@ __host__ __device__ inline int qp_profile_kind(const mpcg_problem& pr) {
 #define MPCG_KERNEL_ATTR __launch_bounds__(64, 1)
 #endif
 // one solve `sol` on the calling wavefront (the body of sqp_kernel)
-template <class C, bool FULL, int PROF>
+template <class C, bool FULL, int PROF, int MODE>
 __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io,
                                           unsigned long long* __restrict__ stamps, double* __restrict__ gws,
-                                          const int sol) {
+                                          const int sol, const int split_it) {
 #include "mpcg_sqp_body.inc"
 }
 
@@ -718,11 +744,19 @@ __device__ __forceinline__ void sqp_solve(mpcg_problem pr, int batch, mpcg_io io
 // solve of the whole batch (the tail).  Every wave leaves the loop on its first
 // ticket >= batch.  launch_instance zeroes the queue words on the launch stream before every
 // launch, so no launch depends on how the previous one on the same workspace ended.
-template <class C, bool FULL = false, int PROF = PROF_RUNTIME>
+// MODE (the split launch, split_on): MODE_LIN linearises RTI iteration split_it, MODE_QP solves its QP and
+// steps; the fused kernel (MODE_FUSED) runs the whole loop
+template <class C, int MODE>
+__host__ __device__ constexpr bool kernel_queue() {
+    return MODE == MODE_FUSED ? C::QUEUE : MODE == MODE_QP ? (MPCG_SPLIT & 2) != 0 : (MPCG_SPLIT & 4) != 0;
+}
+template <class C, bool FULL = false, int PROF = PROF_RUNTIME, int MODE = MODE_FUSED>
 __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io io,
                                                     unsigned long long* __restrict__ stamps,
-                                                    double* __restrict__ gws, unsigned* __restrict__ queue) {
-    if constexpr (!C::QUEUE) {
+                                                    double* __restrict__ gws, unsigned* __restrict__ queue,
+                                                    int split_it) {
+    static_assert(!(FULL && MODE != MODE_FUSED), "the full variant is not split");
+    if constexpr (!kernel_queue<C, MODE>()) {
         (void)queue;
         const int sol = blockIdx.x;
 #include "mpcg_sqp_body.inc"
@@ -743,7 +777,7 @@ __global__ MPCG_KERNEL_ATTR void sqp_kernel(mpcg_problem pr, int batch, mpcg_io 
             return t < (unsigned)batch ? (int)t : batch;
         };
         for (int sol = q ? next() : (int)blockIdx.x; sol < batch; sol = q ? next() : batch) {
-            sqp_solve<C, FULL, PROF>(pr, batch, io, stamps, gws, sol);
+            sqp_solve<C, FULL, PROF, MODE>(pr, batch, io, stamps, gws, sol, split_it);
             wave_sync();
         }
     }

@@ -56,6 +56,13 @@ def main():
                 x, y = ref[k], o[k]
                 same = np.array_equal(x, y, equal_nan=True) if x.dtype.kind == "f" else np.array_equal(x, y)
                 rec[k] = "equal" if same else float(np.nanmax(np.abs(x.astype(np.float64) - y.astype(np.float64))))
+            # the solves whose outputs differ at all (first few listed)
+            bad = np.zeros(len(ref["exit"]), bool)
+            for k in ref.files:
+                x, y = ref[k].reshape(len(bad), -1), o[k].reshape(len(bad), -1)
+                bad |= ~((x == y) | (np.isnan(x) & np.isnan(y)) if x.dtype.kind == "f" else (x == y)).all(axis=1)
+            rec["n_diff_solves"] = int(bad.sum())
+            rec["first_diff"] = [int(i) for i in np.flatnonzero(bad)[:8]]
             print(json.dumps(rec), flush=True)
 
 
